@@ -1,0 +1,162 @@
+/*
+ * stylemc_hip.h -- C ABI of the MI355X (gfx950) kernels for StyleMC's find_direction hot path.
+ *
+ * Conventions (all entry points):
+ *   - extern "C", plain device pointers + explicit sizes, fp32 NCHW-contiguous tensors.
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream).  Kernels are
+ *     enqueued asynchronously; nothing synchronises the host.
+ *   - Return SMC_OK (0) or an SMC_ERR_* code; smc_last_error() returns a thread-local message.
+ *   - The caller owns every buffer.  Nothing allocates device memory internally: ops that need
+ *     scratch space take a `workspace` whose size the matching *_workspace_size() query returns.
+ *   - Pointers documented "may be NULL" mean "absent" (the reference passes empty tensors for that,
+ *     torch_utils/ops/bias_act.py:39,150-157).
+ *
+ * Each entry point cites the reference interface it replaces.
+ */
+#ifndef STYLEMC_HIP_H
+#define STYLEMC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMC_ABI_VERSION 1
+
+#define SMC_OK 0
+#define SMC_ERR_INVALID 1     /* bad argument / shape (reference: TORCH_CHECK -> RuntimeError)   */
+#define SMC_ERR_UNSUPPORTED 2 /* valid request this build has no kernel for                       */
+#define SMC_ERR_LAUNCH 3      /* hipGetLastError() after a launch was not hipSuccess             */
+
+/* activation codes: identical to the reference's cuda_idx (torch_utils/ops/bias_act.py:23-33) */
+#define SMC_ACT_LINEAR 1
+#define SMC_ACT_RELU 2
+#define SMC_ACT_LRELU 3
+#define SMC_ACT_TANH 4
+#define SMC_ACT_SIGMOID 5
+#define SMC_ACT_ELU 6
+#define SMC_ACT_SELU 7
+#define SMC_ACT_SOFTPLUS 8
+#define SMC_ACT_SWISH 9
+
+int smc_abi_version(void);
+const char* smc_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * bias_act -- replaces the pybind `_plugin.bias_act(x, b, xref, yref, dy, grad, dim, act, alpha,
+ * gain, clamp)` of torch_utils/ops/bias_act.cpp:32-90 (called at bias_act.py:153,182,201).
+ *   bias index of element i = (i / step_b) % size_b   (step_b = x.stride(dim), size_b = b.numel())
+ *   grad 0: y = clamp(act(x + b) * gain)
+ *   grad 1: y = d/dx   (x holds the incoming gradient, xref/yref the saved forward tensors)
+ *   grad 2: second-order term (only for activations with a 2nd derivative)
+ * b, xref, yref, dy may be NULL.  clamp < 0 disables clamping.
+ */
+int smc_bias_act_f32(const float* x, const float* b, const float* xref, const float* yref, const float* dy,
+                     float* y, int64_t numel, int64_t size_b, int64_t step_b, int grad, int act, float alpha,
+                     float gain, float clamp, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * upfirdn2d -- replaces `_plugin.upfirdn2d(x, f, upx, upy, downx, downy, padx0, padx1, pady0, pady1,
+ * flip, gain)` of torch_utils/ops/upfirdn2d.cpp:16-94 (called at upfirdn2d.py:237-240).
+ *   x [major, in_h, in_w], f [fh, fw] (device fp32), y [major, out_h, out_w] with
+ *   out_h = (in_h*upy + pady0 + pady1 - fh + downy) / downy  (checked).
+ *   flip = 0: convolution (taps flipped), 1: correlation.  Negative padding crops.
+ */
+int smc_upfirdn2d_f32(const float* x, const float* f, float* y, int64_t major, int in_h, int in_w, int out_h,
+                      int out_w, int fh, int fw, int upx, int upy, int downx, int downy, int padx0, int padx1,
+                      int pady0, int pady1, int flip, float gain, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Modulated convolution (replaces the cuDNN grouped F.conv2d / F.conv_transpose2d of
+ * torch_utils/ops/conv2d_resample.py:29-54,125-147 driven by the upstream modulated_conv2d).
+ * The build uses the non-fused form: x*s -> shared-weight conv -> *d[n,o] -> +noise -> bias_act,
+ * mathematically identical to the reference's fused grouped conv, without per-sample weights.
+ *
+ * smc_conv_gemm_f32 is an implicit-GEMM "gather convolution" on MFMA (v_mfma_f32_32x32x2_f32):
+ *   for every phase p, output position (a, b) in [0,out_h) x [0,out_w) of sample n:
+ *     acc[n,o,a,b] = sum_{t < ntaps, i < cin} W_p[t][i][o] * s[n,i] * x[n, i, a*in_stride + tap_dy[t],
+ *                                                                      b*in_stride + tap_dx[t]]
+ *   (out-of-range input reads are 0), written to y[n, o, out_oy + out_sy*a, out_ox + out_sx*b]
+ *   through the epilogue.  One phase = a plain (strided) conv; four phases = the polyphase
+ *   stride-2 transposed conv of the up=2 layers.
+ */
+typedef struct {
+    int ntaps;            /* 1..9                                             */
+    int tap_dy[9];
+    int tap_dx[9];
+    int in_stride;        /* 1 or 2                                           */
+    int out_h, out_w;     /* output grid of this phase                        */
+    int out_oy, out_ox;   /* offset of the grid in y                          */
+    int out_sy, out_sx;   /* stride of the grid in y                          */
+    const float* wk;      /* [ntaps][cin][cout] packed weights                */
+} smc_conv_phase;
+
+#define SMC_EPI_STORE 0   /* y = acc                                                           */
+#define SMC_EPI_MODACT 1  /* u = acc; y = clamp(act(u*d[n,o] + noise*strength + bias[o])*gain)  */
+
+typedef struct {
+    int mode;                      /* SMC_EPI_*                                                  */
+    const float* d;                /* [n][cout] demodulation coefficients, may be NULL (=1)       */
+    const float* noise;            /* may be NULL; element = noise[n*noise_nstride + y*W + x]     */
+    int64_t noise_nstride;         /* 0 for the const [H, W] noise buffer                          */
+    const float* noise_strength;   /* device scalar, may be NULL (=1)                             */
+    const float* bias;             /* [cout], may be NULL                                          */
+    int act;                       /* SMC_ACT_* (linear / relu / lrelu on this path)               */
+    float alpha, gain, clamp;      /* clamp < 0: none                                              */
+    float* u_save;                 /* may be NULL: stores u (pre-demod acc), layout of y            */
+} smc_conv_epilogue;
+
+/* bytes of workspace smc_conv_gemm_f32 needs for these sizes (0 = none). */
+int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, int y_w, const smc_conv_phase* phases,
+                                     int nphases);
+
+int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h, int y_w,
+                      const smc_conv_phase* phases, int nphases, const float* s_in, const smc_conv_epilogue* epi,
+                      float* workspace, int64_t workspace_bytes, void* stream);
+
+/* Apply the modconv epilogue to a raw accumulator tensor, summing `nsplit` partial planes
+ * (src + k*split_stride).  src/y/u_save: [n, c, h, w]. */
+int smc_modconv_epilogue_f32(const float* src, int nsplit, int64_t split_stride, float* y, int n, int c, int h,
+                             int w, const smc_conv_epilogue* epi, void* stream);
+
+/* Fused conv0 epilogue: U = upfirdn2d(T, f, pad=(padx0,pady0 on both sides), gain=fgain) (1:1 FIR),
+ * then the modconv epilogue (u_save receives U).  T: [n, c, t_h, t_w] (may be `nsplit` partial
+ * planes), y: [n, c, y_h, y_w].  Only the 4x4 FIR of the [1,3,3,1] resample filter has a fused kernel;
+ * other sizes return SMC_ERR_UNSUPPORTED. */
+int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_stride, float* y, int n, int c, int t_h,
+                             int t_w, int y_h, int y_w, const float* f, int fh, int fw, int padx0, int pady0,
+                             float fgain, int flip, const smc_conv_epilogue* epi, void* stream);
+
+/* d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps), wsq[o,i] = sum_k W[o,i,k]^2 (demodulation). */
+int smc_modconv_demod_f32(const float* s, const float* wsq, float* d, int n, int cin, int cout, float eps,
+                          void* stream);
+
+/* Backward of the modconv epilogue: recompute y from u, dz = bias_act grad (CUDA-kernel semantics,
+ * bias_act.cu:51-142), du = dz * d[n,o]; if dd != NULL: dd[n,o] += sum_hw dz*u. */
+int smc_modconv_act_bwd_f32(const float* g, const float* u, float* du, float* dd, int n, int c, int h, int w,
+                            const smc_conv_epilogue* epi, void* stream);
+
+/* out[r] (+)= sum_p a[r,p]*b[r,p] over rows r < rows of length len; if a_scaled != NULL also
+ * a_scaled[r,p] = a[r,p]*scale[r] (scale may be NULL only when a_scaled is NULL). */
+int smc_channel_dot_f32(const float* a, const float* b, const float* scale, float* out, float* a_scaled,
+                        int64_t rows, int64_t len, int accumulate, void* stream);
+
+/* ds[n,i] += -s[n,i] * sum_o dd[n,o] * d[n,o]^3 * wsq[o,i]   (gradient through the demodulation). */
+int smc_modconv_demod_bwd_f32(const float* s, const float* d, const float* dd, const float* wsq, float* ds, int n,
+                              int cin, int cout, void* stream);
+
+/* ToRGB (1x1 modulated conv without demodulation + linear bias_act with clamp), replacing the
+ * [upstream] ToRGBLayer.forward path (utils.py:47):  y[n,c,p] = clamp(sum_i w[c,i]*s[n,i]*x[n,i,p] + b[c]).
+ * w: [cout][cin], s: [n][cin] (already multiplied by the layer's weight_gain), b: [cout] or NULL. */
+int smc_torgb_fwd_f32(const float* x, const float* w, const float* s, const float* b, float* y, int n, int cin,
+                      int cout, int h, int w_, float clamp, void* stream);
+
+/* dx[n,i,p] (+)= (scale ? s[n,i] : 1) * sum_c w[c,i] * g[n,c,p] * [|y[n,c,p]| < clamp] */
+int smc_torgb_bwd_f32(const float* g, const float* y, const float* w, const float* s, float* dx, int n, int cin,
+                      int cout, int h, int w_, float clamp, int scale, int accumulate, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STYLEMC_HIP_H */

@@ -1,0 +1,149 @@
+"""ctypes binding of the C ABI in ``include/stylemc_hip.h`` (``stylemc_amd/_lib/libstylemc_hip.so``).
+
+The library is loaded after ``import torch`` so its ``libamdhip64.so.7`` dependency resolves to the
+HIP runtime torch already loaded (one runtime, so torch's streams are valid handles here).
+There is no fallback: if the library is missing or a call fails, a RuntimeError is raised.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SMC_HIP_LIB", os.path.join(PKG, "_lib", "libstylemc_hip.so"))
+
+c_int, c_int64, c_float, c_void_p, c_char_p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_char_p
+
+ACT_CODES = {"linear": 1, "relu": 2, "lrelu": 3, "tanh": 4, "sigmoid": 5, "elu": 6, "selu": 7, "softplus": 8,
+             "swish": 9}
+EPI_STORE, EPI_MODACT = 0, 1
+
+
+class ConvPhase(ctypes.Structure):
+    _fields_ = [("ntaps", c_int), ("tap_dy", c_int * 9), ("tap_dx", c_int * 9), ("in_stride", c_int),
+                ("out_h", c_int), ("out_w", c_int), ("out_oy", c_int), ("out_ox", c_int), ("out_sy", c_int),
+                ("out_sx", c_int), ("wk", c_void_p)]
+
+
+class ConvEpilogue(ctypes.Structure):
+    _fields_ = [("mode", c_int), ("d", c_void_p), ("noise", c_void_p), ("noise_nstride", c_int64),
+                ("noise_strength", c_void_p), ("bias", c_void_p), ("act", c_int), ("alpha", c_float),
+                ("gain", c_float), ("clamp", c_float), ("u_save", c_void_p)]
+
+
+P = c_void_p
+_SIGS = {
+    "smc_abi_version": (c_int, []),
+    "smc_last_error": (c_char_p, []),
+    "smc_bias_act_f32": (c_int, [P, P, P, P, P, P, c_int64, c_int64, c_int64, c_int, c_int, c_float, c_float, c_float,
+                                 P]),
+    "smc_upfirdn2d_f32": (c_int, [P, P, P, c_int64] + [c_int] * 15 + [c_float, P]),
+    "smc_conv_gemm_workspace_size": (c_int64, [c_int, c_int, c_int, c_int, c_int, P, c_int]),
+    "smc_conv_gemm_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, c_int64,
+                                  P]),
+    "smc_modconv_epilogue_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, P, P]),
+    "smc_modconv_blur_act_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int,
+                                         c_int, c_int, c_int, c_float, c_int, P, P]),
+    "smc_modconv_demod_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
+    "smc_modconv_act_bwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P]),
+    "smc_channel_dot_f32": (c_int, [P, P, P, P, P, c_int64, c_int64, c_int, P]),
+    "smc_modconv_demod_bwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, P]),
+    "smc_torgb_fwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, P]),
+    "smc_torgb_bwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def exported_symbols():
+    return sorted(_SIGS)
+
+
+def load(path=None):
+    """Load (once) and return the ctypes library; raises if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RuntimeError(f"stylemc_amd: HIP kernel library not found at {p}; build it with "
+                               f"`python -m stylemc_amd.build` (there is no CPU fallback)")
+        lib = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.smc_abi_version() != 1:
+            raise RuntimeError("stylemc_amd: ABI version mismatch, rebuild the library")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc, name):
+    if rc != 0:
+        msg = load().smc_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (code {rc}): {msg}")
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args), name)
+
+
+def ptr(t):
+    """Device pointer of an fp32 CUDA tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("stylemc_amd kernels run on the GPU only (got a CPU tensor)")
+    if t.dtype != torch.float32:
+        raise NotImplementedError(f"stylemc_amd kernels are fp32-only (got {t.dtype})")
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+# --------------------------------------------------------------------------------- launch timing
+
+class KernelTimer:
+    """Records HIP events around selected launches (bench.py's live roofline measurement)."""
+
+    def __init__(self, family):
+        self.family = family
+        self.records = []  # (start_event, end_event, flops)
+
+    def wrap(self, flops):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        return s, e, flops
+
+    def finish(self, token):
+        s, e, flops = token
+        e.record()
+        self.records.append((s, e, flops))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        times = [s.elapsed_time(e) * 1e-3 for s, e, _ in self.records]
+        flops = [f for _, _, f in self.records]
+        return {"launches": len(times), "seconds": sum(times), "flops": sum(flops)}
+
+
+_timer = None
+
+
+def set_timer(timer):
+    global _timer
+    _timer = timer
+
+
+def timer():
+    return _timer

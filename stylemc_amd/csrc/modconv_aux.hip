@@ -1,0 +1,302 @@
+// Memory-bound companions of the modconv GEMM for gfx950:
+//   * split-K reduction + modconv epilogue            (smc_modconv_epilogue_f32)
+//   * conv0's fused 4x4 blur + modconv epilogue       (smc_modconv_blur_act_f32)
+//   * demodulation d = rsqrt(s^2 . Wsq + eps)         (smc_modconv_demod_f32, one wave per (n,o),
+//                                                       wavefront-shuffle reduction)
+//   * epilogue backward + d-gradient reduction        (smc_modconv_act_bwd_f32)
+//   * per-channel dot products for style gradients    (smc_channel_dot_f32)
+//   * gradient through the demodulation               (smc_modconv_demod_bwd_f32)
+// The forward replaces the bias_act / upfirdn2d / fma launches the reference issues after each
+// grouped conv ([upstream] SynthesisLayer.forward -> bias_act.py:153, upfirdn2d.py:237, fma.py:15).
+#include "common.hpp"
+
+namespace {
+
+struct Epi {
+    int mode;
+    const float* d;
+    const float* noise;
+    int64_t noise_nstride;
+    const float* noise_strength;
+    const float* bias;
+    int act;
+    float alpha, gain, clamp;
+    float* u_save;
+};
+
+Epi to_epi(const smc_conv_epilogue* e) {
+    Epi r{};
+    r.mode = SMC_EPI_STORE;
+    r.act = SMC_ACT_LINEAR;
+    r.gain = 1.f;
+    r.clamp = -1.f;
+    if (e) {
+        r.mode = e->mode; r.d = e->d; r.noise = e->noise; r.noise_nstride = e->noise_nstride;
+        r.noise_strength = e->noise_strength; r.bias = e->bias; r.act = e->act; r.alpha = e->alpha;
+        r.gain = e->gain; r.clamp = e->clamp; r.u_save = e->u_save;
+    }
+    return r;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Block-wide sum of 256 threads; result valid in every thread.
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+
+// ---------------------------------------------------------------------------------------------- epilogue
+
+__global__ __launch_bounds__(256) void epilogue_kernel(const float* src, int nsplit, int64_t split_stride, float* y,
+                                                       int c, int64_t hw, int64_t total, Epi e) {
+    const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
+        float v = src[idx];
+        for (int s = 1; s < nsplit; ++s) v += src[s * split_stride + idx];
+        if (e.mode == SMC_EPI_STORE) {
+            y[idx] = v;
+            continue;
+        }
+        const int64_t nc = idx / hw;
+        const int64_t pix = idx - nc * hw;
+        const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
+        if (e.u_save) e.u_save[idx] = v;
+        const float nz = e.noise ? e.noise[n * e.noise_nstride + pix] * nstr : 0.f;
+        y[idx] = smc::epi_y(v, e.d ? e.d[nc] : 1.f, nz, e.bias ? e.bias[o] : 0.f, e.act, e.alpha, e.gain, e.clamp);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------- blur + act
+
+constexpr int kBT = 32;        // output tile (kBT x kBT), 256 threads x 4 rows
+constexpr int kMaxF = 8;
+
+__global__ __launch_bounds__(256) void blur_act_kernel(const float* t, int nsplit, int64_t split_stride, float* y,
+                                                       int c, int t_h, int t_w, int y_h, int y_w, const float* f,
+                                                       int fh, int fw, int padx0, int pady0, float fgain, int flip,
+                                                       Epi e) {
+    __shared__ float tile[(kBT + kMaxF - 1) * (kBT + kMaxF - 1)];
+    __shared__ float taps[kMaxF * kMaxF];
+    const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
+    const int ox0 = blockIdx.x * kBT, oy0 = blockIdx.y * kBT;
+    const int64_t nc = blockIdx.z;
+    const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
+    if (tid < fh * fw) {
+        const int jy = tid / fw, jx = tid % fw;
+        taps[tid] = f[(flip ? jy : fh - 1 - jy) * fw + (flip ? jx : fw - 1 - jx)] * fgain;
+    }
+    const int rows = kBT + fh - 1, cols = kBT + fw - 1;
+    const int iy0 = oy0 - pady0, ix0 = ox0 - padx0;
+    const float* tp = t + nc * (int64_t)t_h * t_w;
+    for (int i = tid; i < rows * cols; i += 256) {
+        const int r = i / cols, cc = i - r * cols;
+        const int iy = iy0 + r, ix = ix0 + cc;
+        float v = 0.f;
+        if (iy >= 0 && iy < t_h && ix >= 0 && ix < t_w) {
+            const int64_t off = (int64_t)iy * t_w + ix;
+            v = tp[off];
+            for (int s = 1; s < nsplit; ++s) v += tp[s * split_stride + off];
+        }
+        tile[i] = v;
+    }
+    __syncthreads();
+    const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
+    const float dv = e.d ? e.d[nc] : 1.f;
+    const float bv = e.bias ? e.bias[o] : 0.f;
+    const int ox = ox0 + tx;
+    if (ox >= y_w) return;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int oy = oy0 + ty + 8 * k;
+        if (oy >= y_h) continue;
+        const int ly = ty + 8 * k;
+        float u = 0.f;
+        for (int jy = 0; jy < fh; ++jy) {
+            const float* trow = tile + (ly + jy) * cols + tx;
+            const float* frow = taps + jy * fw;
+            for (int jx = 0; jx < fw; ++jx) u += frow[jx] * trow[jx];
+        }
+        const int64_t pix = (int64_t)oy * y_w + ox;
+        const int64_t idx = nc * (int64_t)y_h * y_w + pix;
+        if (e.mode == SMC_EPI_STORE) {
+            y[idx] = u;
+            continue;
+        }
+        if (e.u_save) e.u_save[idx] = u;
+        const float nz = e.noise ? e.noise[n * e.noise_nstride + pix] * nstr : 0.f;
+        y[idx] = smc::epi_y(u, dv, nz, bv, e.act, e.alpha, e.gain, e.clamp);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------- demod
+
+__global__ __launch_bounds__(256) void demod_kernel(const float* s, const float* wsq, float* d, int n, int cin,
+                                                    int cout, float eps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per (n, o)
+    if (row >= (int64_t)n * cout) return;
+    const int nn = (int)(row / cout), o = (int)(row - (int64_t)nn * cout);
+    const float* sp = s + (int64_t)nn * cin;
+    const float* wp = wsq + (int64_t)o * cin;
+    float acc = 0.f;
+    for (int i = lane; i < cin; i += 64) {
+        const float sv = sp[i];
+        acc += sv * sv * wp[i];
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) d[row] = rsqrtf(acc + eps);
+}
+
+// ---------------------------------------------------------------------------------------------- act bwd
+
+__global__ __launch_bounds__(256) void act_bwd_kernel(const float* g, const float* u, float* du, float* dd, int c,
+                                                      int64_t hw, Epi e) {
+    __shared__ float red[4];
+    const int64_t nc = blockIdx.y;
+    const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
+    const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
+    const float dv = e.d ? e.d[nc] : 1.f;
+    const float bv = e.bias ? e.bias[o] : 0.f;
+    const int64_t base = nc * hw;
+    float part = 0.f;
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < hw; p += (int64_t)gridDim.x * 256) {
+        const float uv = u[base + p];
+        const float nz = e.noise ? e.noise[n * e.noise_nstride + p] * nstr : 0.f;
+        const float yv = smc::epi_y(uv, dv, nz, bv, e.act, e.alpha, e.gain, e.clamp);
+        const float dz = smc::act_grad_y(e.act, g[base + p], yv, e.alpha, e.gain, e.clamp);
+        du[base + p] = dz * dv;
+        part += dz * uv;
+    }
+    if (dd) {
+        const float tot = block_sum256(part, red);
+        if (threadIdx.x == 0) atomicAdd(dd + nc, tot);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------- channel dot
+
+__global__ __launch_bounds__(256) void channel_dot_kernel(const float* a, const float* b, const float* scale,
+                                                          float* out, float* a_scaled, int64_t len, int accumulate) {
+    __shared__ float red[4];
+    const int64_t r = blockIdx.x;
+    const float* ap = a + r * len;
+    const float* bp = b + r * len;
+    const float sc = scale ? scale[r] : 1.f;
+    float acc = 0.f;
+    for (int64_t p = threadIdx.x; p < len; p += 256) {
+        const float av = ap[p];
+        acc += av * bp[p];
+        if (a_scaled) a_scaled[r * len + p] = av * sc;
+    }
+    const float tot = block_sum256(acc, red);
+    if (threadIdx.x == 0) out[r] = accumulate ? out[r] + tot : tot;
+}
+
+// ---------------------------------------------------------------------------------------------- demod bwd
+
+__global__ __launch_bounds__(256) void demod_bwd_kernel(const float* s, const float* d, const float* dd,
+                                                        const float* wsq, float* ds, int cin, int cout) {
+    __shared__ float coef[256];
+    const int nn = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    float acc = 0.f;
+    for (int o0 = 0; o0 < cout; o0 += 256) {
+        __syncthreads();
+        const int o = o0 + threadIdx.x;
+        if (o < cout) {
+            const float dv = d[(int64_t)nn * cout + o];
+            coef[threadIdx.x] = dd[(int64_t)nn * cout + o] * dv * dv * dv;
+        }
+        __syncthreads();
+        const int lim = cout - o0 < 256 ? cout - o0 : 256;
+        if (i < cin)
+            for (int k = 0; k < lim; ++k) acc += coef[k] * wsq[(int64_t)(o0 + k) * cin + i];
+    }
+    if (i < cin) ds[(int64_t)nn * cin + i] += -s[(int64_t)nn * cin + i] * acc;
+}
+
+int64_t grid_cap(int64_t blocks) {
+    const int64_t cap = (int64_t)smc::device_cu_count() * 16;
+    if (blocks > cap) blocks = cap;
+    return blocks < 1 ? 1 : blocks;
+}
+
+}  // namespace
+
+SMC_API int smc_modconv_epilogue_f32(const float* src, int nsplit, int64_t split_stride, float* y, int n, int c, int h,
+                                     int w, const smc_conv_epilogue* epi, void* stream) {
+    SMC_CHECK(src && y && n >= 1 && c >= 1 && h >= 1 && w >= 1 && nsplit >= 1, "smc_modconv_epilogue_f32: bad args");
+    const int64_t total = (int64_t)n * c * h * w;
+    hipLaunchKernelGGL(epilogue_kernel, dim3((unsigned)grid_cap(smc::ceil_div(total, 256))), dim3(256), 0,
+                       smc::as_stream(stream), src, nsplit, split_stride, y, c, (int64_t)h * w, total, to_epi(epi));
+    return smc::check_launch("smc_modconv_epilogue_f32");
+}
+
+SMC_API int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_stride, float* y, int n, int c,
+                                     int t_h, int t_w, int y_h, int y_w, const float* f, int fh, int fw, int padx0,
+                                     int pady0, float fgain, int flip, const smc_conv_epilogue* epi, void* stream) {
+    SMC_CHECK(t && y && f && n >= 1 && c >= 1 && nsplit >= 1, "smc_modconv_blur_act_f32: bad args");
+    if (fh > kMaxF || fw > kMaxF || fh < 1 || fw < 1) {
+        smc::set_error("smc_modconv_blur_act_f32: filter %dx%d > %dx%d", fh, fw, kMaxF, kMaxF);
+        return SMC_ERR_UNSUPPORTED;
+    }
+    SMC_CHECK(y_h >= 1 && y_w >= 1 && y_h <= t_h + 2 * pady0 && y_w <= t_w + 2 * padx0,
+              "smc_modconv_blur_act_f32: bad output size");
+    SMC_CHECK((int64_t)n * c < 65536, "smc_modconv_blur_act_f32: too many planes");
+    dim3 grid((unsigned)smc::ceil_div(y_w, kBT), (unsigned)smc::ceil_div(y_h, kBT), (unsigned)(n * c));
+    hipLaunchKernelGGL(blur_act_kernel, grid, dim3(256), 0, smc::as_stream(stream), t, nsplit, split_stride, y, c,
+                       t_h, t_w, y_h, y_w, f, fh, fw, padx0, pady0, fgain, flip, to_epi(epi));
+    return smc::check_launch("smc_modconv_blur_act_f32");
+}
+
+SMC_API int smc_modconv_demod_f32(const float* s, const float* wsq, float* d, int n, int cin, int cout, float eps,
+                                  void* stream) {
+    SMC_CHECK(s && wsq && d && n >= 1 && cin >= 1 && cout >= 1, "smc_modconv_demod_f32: bad args");
+    const int64_t rows = (int64_t)n * cout;
+    hipLaunchKernelGGL(demod_kernel, dim3((unsigned)smc::ceil_div(rows, 4)), dim3(256), 0, smc::as_stream(stream), s,
+                       wsq, d, n, cin, cout, eps);
+    return smc::check_launch("smc_modconv_demod_f32");
+}
+
+SMC_API int smc_modconv_act_bwd_f32(const float* g, const float* u, float* du, float* dd, int n, int c, int h, int w,
+                                    const smc_conv_epilogue* epi, void* stream) {
+    SMC_CHECK(g && u && du && n >= 1 && c >= 1 && h >= 1 && w >= 1, "smc_modconv_act_bwd_f32: bad args");
+    SMC_CHECK(epi && epi->mode == SMC_EPI_MODACT, "smc_modconv_act_bwd_f32: needs a MODACT epilogue");
+    const int64_t hw = (int64_t)h * w;
+    const int64_t planes = (int64_t)n * c;
+    int64_t per_plane = smc::ceil_div(hw, 256 * 8);  // ~8 elements per thread
+    if (per_plane < 1) per_plane = 1;
+    SMC_CHECK(planes < 65536, "smc_modconv_act_bwd_f32: too many planes");
+    hipLaunchKernelGGL(act_bwd_kernel, dim3((unsigned)per_plane, (unsigned)planes), dim3(256), 0,
+                       smc::as_stream(stream), g, u, du, dd, c, hw, to_epi(epi));
+    return smc::check_launch("smc_modconv_act_bwd_f32");
+}
+
+SMC_API int smc_channel_dot_f32(const float* a, const float* b, const float* scale, float* out, float* a_scaled,
+                                int64_t rows, int64_t len, int accumulate, void* stream) {
+    SMC_CHECK(a && b && out && rows >= 1 && len >= 1, "smc_channel_dot_f32: bad args");
+    SMC_CHECK(!a_scaled || scale, "smc_channel_dot_f32: a_scaled needs scale");
+    SMC_CHECK(rows < (1LL << 31), "smc_channel_dot_f32: too many rows");
+    hipLaunchKernelGGL(channel_dot_kernel, dim3((unsigned)rows), dim3(256), 0, smc::as_stream(stream), a, b, scale,
+                       out, a_scaled, len, accumulate);
+    return smc::check_launch("smc_channel_dot_f32");
+}
+
+SMC_API int smc_modconv_demod_bwd_f32(const float* s, const float* d, const float* dd, const float* wsq, float* ds,
+                                      int n, int cin, int cout, void* stream) {
+    SMC_CHECK(s && d && dd && wsq && ds && n >= 1 && cin >= 1 && cout >= 1, "smc_modconv_demod_bwd_f32: bad args");
+    SMC_CHECK(n < 65536, "smc_modconv_demod_bwd_f32: batch too large");
+    hipLaunchKernelGGL(demod_bwd_kernel, dim3((unsigned)smc::ceil_div(cin, 256), (unsigned)n), dim3(256), 0,
+                       smc::as_stream(stream), s, d, dd, wsq, ds, cin, cout);
+    return smc::check_launch("smc_modconv_demod_bwd_f32");
+}

@@ -1,0 +1,156 @@
+// ToRGB for gfx950: 1x1 modulated conv without demodulation + linear bias_act (clamped).
+//
+// Replaces the [upstream] ToRGBLayer.forward path (modulated_conv2d(demodulate=False) -> cuDNN 1x1
+// grouped conv, conv2d_resample.py:29-54, then bias_act.py:153) called at utils.py:47.  With 3 output
+// channels this is an HBM-bound channel reduction, not a GEMM: each thread streams one float4 of
+// positions through all input channels, the [3 x cin] modulated weights of its sample sit in LDS.
+#include "common.hpp"
+
+namespace {
+
+constexpr int kMaxOut = 4;
+constexpr int kMaxIn = 1024;
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void torgb_fwd_kernel(const float* x, const float* w, const float* s, const float* b,
+                                                        float* y, int cin, int cout, int64_t hw, float clamp) {
+    __shared__ float ws[kMaxOut * kMaxIn];
+    const int nn = blockIdx.y;
+    for (int i = threadIdx.x; i < cout * cin; i += 256) {
+        const int c = i / cin, k = i - c * cin;
+        ws[i] = w[i] * s[(int64_t)nn * cin + k];
+    }
+    __syncthreads();
+    const float* xp = x + (int64_t)nn * cin * hw;
+    float* yp = y + (int64_t)nn * cout * hw;
+    constexpr int V = VEC ? 4 : 1;
+    const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
+    if (p0 >= hw) return;
+    float acc[kMaxOut][V];
+#pragma unroll
+    for (int c = 0; c < kMaxOut; ++c)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[c][v] = 0.f;
+    for (int k = 0; k < cin; ++k) {
+        float xv[V];
+        if (VEC) {
+            const float4 t = *reinterpret_cast<const float4*>(xp + (int64_t)k * hw + p0);
+            xv[0] = t.x; xv[V > 1 ? 1 : 0] = t.y; xv[V > 2 ? 2 : 0] = t.z; xv[V > 3 ? 3 : 0] = t.w;
+        } else {
+            xv[0] = xp[(int64_t)k * hw + p0];
+        }
+#pragma unroll
+        for (int c = 0; c < kMaxOut; ++c) {
+            if (c >= cout) break;
+            const float wv = ws[c * cin + k];
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[c][v] += wv * xv[v];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < kMaxOut; ++c) {
+        if (c >= cout) break;
+        const float bv = b ? b[c] : 0.f;
+        float r[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) r[v] = smc::clamp_fwd(acc[c][v] + bv, clamp);
+        if (VEC) *reinterpret_cast<float4*>(yp + (int64_t)c * hw + p0) = make_float4(r[0], r[V > 1 ? 1 : 0],
+                                                                                      r[V > 2 ? 2 : 0], r[V > 3 ? 3 : 0]);
+        else yp[(int64_t)c * hw + p0] = r[0];
+    }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void torgb_bwd_kernel(const float* g, const float* y, const float* w, const float* s,
+                                                        float* dx, int cin, int cout, int64_t hw, float clamp,
+                                                        int scale, int accumulate) {
+    __shared__ float ws[kMaxOut * kMaxIn];
+    const int nn = blockIdx.y;
+    for (int i = threadIdx.x; i < cout * cin; i += 256) {
+        const int c = i / cin, k = i - c * cin;
+        ws[i] = w[i] * (scale ? s[(int64_t)nn * cin + k] : 1.f);
+    }
+    __syncthreads();
+    constexpr int V = VEC ? 4 : 1;
+    const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
+    if (p0 >= hw) return;
+    float gm[kMaxOut][V];
+#pragma unroll
+    for (int c = 0; c < kMaxOut; ++c) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) gm[c][v] = 0.f;
+        if (c >= cout) continue;
+        const int64_t off = ((int64_t)nn * cout + c) * hw + p0;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const float yv = y[off + v];
+            const bool pass = clamp < 0.f || (yv > -clamp && yv < clamp);  // bias_act.cu:136-141 (grad=1)
+            gm[c][v] = pass ? g[off + v] : 0.f;
+        }
+    }
+    float* dp = dx + (int64_t)nn * cin * hw + p0;
+    for (int k = 0; k < cin; ++k) {
+        float r[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) r[v] = 0.f;
+#pragma unroll
+        for (int c = 0; c < kMaxOut; ++c) {
+            if (c >= cout) break;
+            const float wv = ws[c * cin + k];
+#pragma unroll
+            for (int v = 0; v < V; ++v) r[v] += wv * gm[c][v];
+        }
+        float* dst = dp + (int64_t)k * hw;
+        if (VEC) {
+            float4 o = make_float4(r[0], r[V > 1 ? 1 : 0], r[V > 2 ? 2 : 0], r[V > 3 ? 3 : 0]);
+            if (accumulate) {
+                const float4 prev = *reinterpret_cast<const float4*>(dst);
+                o.x += prev.x; o.y += prev.y; o.z += prev.z; o.w += prev.w;
+            }
+            *reinterpret_cast<float4*>(dst) = o;
+        } else {
+            dst[0] = accumulate ? dst[0] + r[0] : r[0];
+        }
+    }
+}
+
+}  // namespace
+
+SMC_API int smc_torgb_fwd_f32(const float* x, const float* w, const float* s, const float* b, float* y, int n, int cin,
+                              int cout, int h, int w_, float clamp, void* stream) {
+    SMC_CHECK(x && w && s && y && n >= 1 && cin >= 1 && h >= 1 && w_ >= 1, "smc_torgb_fwd_f32: bad args");
+    SMC_CHECK(n < 65536, "smc_torgb_fwd_f32: batch too large");
+    if (cout < 1 || cout > kMaxOut || cin > kMaxIn) {
+        smc::set_error("smc_torgb_fwd_f32: cout=%d (max %d) cin=%d (max %d)", cout, kMaxOut, cin, kMaxIn);
+        return SMC_ERR_UNSUPPORTED;
+    }
+    const int64_t hw = (int64_t)h * w_;
+    const bool vec = hw % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+    const int64_t per = vec ? hw / 4 : hw;
+    dim3 grid((unsigned)smc::ceil_div(per, 256), (unsigned)n);
+    if (vec) hipLaunchKernelGGL(torgb_fwd_kernel<true>, grid, dim3(256), 0, smc::as_stream(stream), x, w, s, b, y, cin,
+                                cout, hw, clamp);
+    else hipLaunchKernelGGL(torgb_fwd_kernel<false>, grid, dim3(256), 0, smc::as_stream(stream), x, w, s, b, y, cin,
+                            cout, hw, clamp);
+    return smc::check_launch("smc_torgb_fwd_f32");
+}
+
+SMC_API int smc_torgb_bwd_f32(const float* g, const float* y, const float* w, const float* s, float* dx, int n, int cin,
+                              int cout, int h, int w_, float clamp, int scale, int accumulate, void* stream) {
+    SMC_CHECK(g && y && w && dx && n >= 1 && cin >= 1 && h >= 1 && w_ >= 1, "smc_torgb_bwd_f32: bad args");
+    SMC_CHECK(!scale || s, "smc_torgb_bwd_f32: scale needs s");
+    SMC_CHECK(n < 65536, "smc_torgb_bwd_f32: batch too large");
+    if (cout < 1 || cout > kMaxOut || cin > kMaxIn) {
+        smc::set_error("smc_torgb_bwd_f32: cout=%d (max %d) cin=%d (max %d)", cout, kMaxOut, cin, kMaxIn);
+        return SMC_ERR_UNSUPPORTED;
+    }
+    const int64_t hw = (int64_t)h * w_;
+    const bool vec = hw % 4 == 0 && (reinterpret_cast<uintptr_t>(dx) & 15) == 0;
+    const int64_t per = vec ? hw / 4 : hw;
+    dim3 grid((unsigned)smc::ceil_div(per, 256), (unsigned)n);
+    if (vec) hipLaunchKernelGGL(torgb_bwd_kernel<true>, grid, dim3(256), 0, smc::as_stream(stream), g, y, w, s, dx, cin,
+                                cout, hw, clamp, scale, accumulate);
+    else hipLaunchKernelGGL(torgb_bwd_kernel<false>, grid, dim3(256), 0, smc::as_stream(stream), g, y, w, s, dx, cin,
+                            cout, hw, clamp, scale, accumulate);
+    return smc::check_launch("smc_torgb_bwd_f32");
+}

@@ -1,0 +1,287 @@
+"""Modulated convolution on gfx950: forward + analytic backward through the C ABI.
+
+Replaces [upstream] ``modulated_conv2d`` + the bias_act / noise epilogue of ``SynthesisLayer`` /
+``ToRGBLayer`` (the per-layer work of utils.py:32,39-40,47).  The computation is the non-fused form
+
+    u  = conv(x * s[n, i], W)                (one shared-weight implicit GEMM on MFMA, whole batch)
+    y  = clamp(act(u * d[n, o] + noise * strength + b) * gain),   d = rsqrt(s^2 . Wsq + 1e-8)
+
+which is mathematically identical to the reference's fused per-sample grouped convolution
+(conv2d_resample.py:125-147 with groups = batch) and needs no per-sample weights.  up=2 layers run
+the stride-2 transposed conv as 4 polyphase GEMM phases, then the [1,3,3,1] blur fused with the
+epilogue (conv2d_resample.py:125-139 semantics: transposed conv, FIR pad 1, gain 4).
+
+Backward (G is frozen, so no weight gradients):
+    dz  = bias_act'(g; y)                      (CUDA-kernel clamp semantics, bias_act.cu:136-141)
+    du  = dz * d,   dd[n,o] = sum_p dz * u
+    dxs = conv^T(du, W)  [up=2: through the blur adjoint + stride-2 gather conv]
+    dx  = dxs * s,  ds[n,i] = sum_p dxs * x  -  s[n,i] * sum_o dd * d^3 * Wsq[o,i]
+"""
+import ctypes
+
+import torch
+
+from . import _hip
+
+
+def _phase(taps, in_stride, out_h, out_w, out_oy, out_ox, out_sy, out_sx, wk):
+    ph = _hip.ConvPhase()
+    ph.ntaps = len(taps)
+    for t, (dy, dx) in enumerate(taps):
+        ph.tap_dy[t] = dy
+        ph.tap_dx[t] = dx
+    ph.in_stride = in_stride
+    ph.out_h, ph.out_w, ph.out_oy, ph.out_ox, ph.out_sy, ph.out_sx = out_h, out_w, out_oy, out_ox, out_sy, out_sx
+    ph.wk = wk.data_ptr()
+    return ph
+
+
+class PackedConv:
+    """Frozen conv weights repacked for the gather GEMM (K = tap-major x channel, N contiguous)."""
+
+    def __init__(self, weight, up):
+        W = weight.detach().to(torch.float32).contiguous()
+        self.cout, self.cin, kh, kw = W.shape
+        self.k = kh
+        self.up = up
+        if not (kh == kw and kh in (1, 3)) or up not in (1, 2) or (up == 2 and kh != 3):
+            raise NotImplementedError(f"modulated conv: kernel {kh}x{kw} with up={up} has no gfx950 kernel")
+        self.wsq = W.square().sum(dim=[2, 3]).contiguous()                           # [O, I]
+        taps = [(ky, kx) for ky in range(kh) for kx in range(kw)]
+        self.wk_bwd = W.permute(2, 3, 0, 1).reshape(kh * kw, self.cout, self.cin).contiguous()  # [t][o][i]
+        if up == 1:
+            c = kh // 2
+            self.fwd_taps = [(ky - c, kx - c) for ky, kx in taps]
+            self.bwd_taps = [(c - ky, c - kx) for ky, kx in taps]
+            self.wk_fwd = W.permute(2, 3, 1, 0).reshape(kh * kw, self.cin, self.cout).contiguous()  # [t][i][o]
+        else:
+            # polyphase transposed conv: T[o, 2a+py, 2b+px] += x[i, a-(ky-py)/2, b-(kx-px)/2] W[o,i,ky,kx]
+            self.phases = []
+            for py in (0, 1):
+                for px in (0, 1):
+                    sel = [(ky, kx) for ky, kx in taps if ky % 2 == py and kx % 2 == px]
+                    wk = torch.stack([W[:, :, ky, kx].t() for ky, kx in sel]).contiguous()  # [t][i][o]
+                    self.phases.append((py, px, [(-(ky - py) // 2, -(kx - px) // 2) for ky, kx in sel], wk))
+            self.bwd_taps = [(ky, kx) for ky, kx in taps]  # stride-2 gather over dT
+        self._cache = {}
+
+    def fwd_phases(self, h, w):
+        key = ("f", h, w)
+        if key not in self._cache:
+            if self.up == 1:
+                arr = (_hip.ConvPhase * 1)(_phase(self.fwd_taps, 1, h, w, 0, 0, 1, 1, self.wk_fwd))
+                self._cache[key] = (arr, 1, h, w)
+            else:
+                th, tw = 2 * h + 1, 2 * w + 1
+                ph = [_phase(t, 1, (th - py + 1) // 2, (tw - px + 1) // 2, py, px, 2, 2, wk)
+                      for py, px, t, wk in self.phases]
+                self._cache[key] = ((_hip.ConvPhase * 4)(*ph), 4, th, tw)
+        return self._cache[key]
+
+    def bwd_phases(self, h, w):
+        key = ("b", h, w)
+        if key not in self._cache:
+            stride = 1 if self.up == 1 else 2
+            self._cache[key] = ((_hip.ConvPhase * 1)(_phase(self.bwd_taps, stride, h, w, 0, 0, 1, 1, self.wk_bwd)), 1)
+        return self._cache[key]
+
+
+def conv_flops(n, cin, cout, h_out, w_out, taps):
+    return 2.0 * n * cin * cout * h_out * w_out * taps
+
+
+def gemm(x, y, phases, nph, cin, cout, s=None, epi=None, alg_flops=0.0):
+    n, _, ih, iw = x.shape
+    yh, yw = y.shape[2], y.shape[3]
+    lib = _hip.load()
+    ws_bytes = lib.smc_conv_gemm_workspace_size(n, cin, cout, yh, yw, phases, nph)
+    ws = torch.empty(max(ws_bytes // 4, 1), device=x.device, dtype=torch.float32) if ws_bytes > 0 else None
+    tm = _hip.timer()
+    tok = tm.wrap(alg_flops) if tm is not None else None
+    _hip.call("smc_conv_gemm_f32", x.data_ptr(), n, cin, ih, iw, y.data_ptr(), cout, yh, yw, phases, nph,
+              _hip.ptr(s), ctypes.byref(epi) if epi is not None else None, _hip.ptr(ws), ws_bytes, _hip.stream())
+    if tok is not None:
+        tm.finish(tok)
+
+
+def _epilogue(mode, d=None, noise=None, noise_nstride=0, strength=None, bias=None, act="linear", alpha=0.0,
+              gain=1.0, clamp=-1.0, u_save=None):
+    e = _hip.ConvEpilogue()
+    e.mode = mode
+    e.d = _hip.ptr(d)
+    e.noise = _hip.ptr(noise)
+    e.noise_nstride = noise_nstride
+    e.noise_strength = _hip.ptr(strength)
+    e.bias = _hip.ptr(bias)
+    e.act = _hip.ACT_CODES[act]
+    e.alpha, e.gain, e.clamp = float(alpha), float(gain), float(clamp)
+    e.u_save = _hip.ptr(u_save)
+    return e
+
+
+class LayerSpec:
+    """Everything the modconv kernels need about one frozen layer (built once per SynthesisLayer)."""
+
+    def __init__(self, weight, bias, up, resample_filter, demodulate=True, act="lrelu", alpha=0.2):
+        self.packed = PackedConv(weight, up)
+        self.bias = bias.detach().float().contiguous() if bias is not None else None
+        self.up = up
+        self.filter = resample_filter.detach().float().contiguous() if resample_filter is not None else None
+        self.demodulate = demodulate
+        self.act = act
+        self.alpha = alpha
+
+
+def _noise_args(noise):
+    if noise is None:
+        return None, 0
+    noise = noise.contiguous()
+    if noise.ndim == 2:
+        return noise, 0
+    assert noise.ndim == 4 and noise.shape[1] == 1, "noise must be [H, W] or [N, 1, H, W]"
+    return noise, noise.shape[2] * noise.shape[3]
+
+
+class ModConvFn(torch.autograd.Function):
+    """y = modconv_epilogue(conv(x * s, W)); grads w.r.t. x and s only."""
+
+    @staticmethod
+    def forward(ctx, x, styles, spec, noise, strength, gain, clamp):
+        x = x.contiguous()
+        styles = styles.contiguous()
+        P = spec.packed
+        n, cin, h, w = x.shape
+        assert cin == P.cin and styles.shape == (n, cin), (x.shape, styles.shape, P.cin)
+        r_h, r_w = h * spec.up, w * spec.up
+        d = None
+        if spec.demodulate:
+            d = torch.empty(n, P.cout, device=x.device, dtype=torch.float32)
+            _hip.call("smc_modconv_demod_f32", _hip.ptr(styles), _hip.ptr(P.wsq), _hip.ptr(d), n, cin, P.cout, 1e-8,
+                      _hip.stream())
+        save = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        y = torch.empty(n, P.cout, r_h, r_w, device=x.device, dtype=torch.float32)
+        u = torch.empty_like(y) if save else None
+        nz, nstride = _noise_args(noise)
+        epi = _epilogue(_hip.EPI_MODACT, d, nz, nstride, strength, spec.bias, spec.act, spec.alpha, gain, clamp, u)
+        phases, nph, th, tw = P.fwd_phases(h, w)
+        if spec.up == 1:
+            gemm(x, y, phases, nph, cin, P.cout, s=styles, epi=epi,
+                 alg_flops=conv_flops(n, cin, P.cout, r_h, r_w, P.k * P.k))
+        else:
+            t = torch.empty(n, P.cout, th, tw, device=x.device, dtype=torch.float32)
+            gemm(x, t, phases, nph, cin, P.cout, s=styles, epi=_epilogue(_hip.EPI_STORE),
+                 alg_flops=conv_flops(n, cin, P.cout, h, w, 9))
+            f = spec.filter.to(x.device)
+            fh, fw = f.shape
+            _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, P.cout, th, tw, r_h, r_w,
+                      _hip.ptr(f), fh, fw, 1, 1, 4.0, 0, ctypes.byref(epi), _hip.stream())
+        ctx.spec, ctx.gain, ctx.clamp = spec, gain, clamp
+        ctx.noise, ctx.nstride, ctx.strength = nz, nstride, strength
+        ctx.save_for_backward(x, styles, d, u)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, styles, d, u = ctx.saved_tensors
+        spec = ctx.spec
+        P = spec.packed
+        n, cin, h, w = x.shape
+        need_dx, need_ds = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if not (need_dx or need_ds):
+            return None, None, None, None, None, None, None
+        gy = gy.contiguous()
+        du = torch.empty_like(u)
+        dd = torch.zeros(n, P.cout, device=x.device, dtype=torch.float32) if (need_ds and spec.demodulate) else None
+        epi = _epilogue(_hip.EPI_MODACT, d, ctx.noise, ctx.nstride, ctx.strength, spec.bias, spec.act, spec.alpha,
+                        ctx.gain, ctx.clamp)
+        _hip.call("smc_modconv_act_bwd_f32", gy.data_ptr(), u.data_ptr(), du.data_ptr(), _hip.ptr(dd), n, P.cout,
+                  u.shape[2], u.shape[3], ctypes.byref(epi), _hip.stream())
+        g = du
+        if spec.up == 2:
+            f = spec.filter.to(x.device)
+            fh, fw = f.shape
+            th, tw = 2 * h + 1, 2 * w + 1
+            g = torch.empty(n, P.cout, th, tw, device=x.device, dtype=torch.float32)
+            # adjoint of FIR(pad 1, gain 4): pad (fw - 1 - 1) = 2 on both sides, correlation (upfirdn2d.py:251-261)
+            _hip.call("smc_upfirdn2d_f32", du.data_ptr(), _hip.ptr(f), g.data_ptr(), n * P.cout, du.shape[2],
+                      du.shape[3], th, tw, fh, fw, 1, 1, 1, 1, fw - 2, fw - 2, fh - 2, fh - 2, 1, 4.0, _hip.stream())
+        dx = torch.empty_like(x) if need_dx else None
+        dxs = torch.empty_like(x) if need_ds else None
+        if need_dx:
+            ebw = _epilogue(_hip.EPI_MODACT, d=styles, act="linear", u_save=dxs)
+            out = dx
+        else:
+            ebw = _epilogue(_hip.EPI_STORE)
+            out = dxs
+        phases, nph = P.bwd_phases(h, w)
+        gemm(g, out, phases, nph, P.cout, cin, epi=ebw, alg_flops=conv_flops(n, P.cout, cin, h, w, P.k * P.k))
+        ds = None
+        if need_ds:
+            ds = torch.empty(n, cin, device=x.device, dtype=torch.float32)
+            _hip.call("smc_channel_dot_f32", dxs.data_ptr(), x.data_ptr(), None, ds.data_ptr(), None, n * cin, h * w, 0,
+                      _hip.stream())
+            if spec.demodulate:
+                _hip.call("smc_modconv_demod_bwd_f32", styles.data_ptr(), d.data_ptr(), dd.data_ptr(),
+                          P.wsq.data_ptr(), ds.data_ptr(), n, cin, P.cout, _hip.stream())
+        return dx, ds, None, None, None, None, None
+
+
+class ToRGBFn(torch.autograd.Function):
+    """y = clamp(sum_i W[c,i] s[n,i] x[n,i,p] + b[c]) (1x1 modconv, demodulate=False, linear bias_act)."""
+
+    @staticmethod
+    def forward(ctx, x, styles, weight2d, bias, clamp):
+        x = x.contiguous()
+        styles = styles.contiguous()
+        n, cin, h, w = x.shape
+        cout = weight2d.shape[0]
+        y = torch.empty(n, cout, h, w, device=x.device, dtype=torch.float32)
+        _hip.call("smc_torgb_fwd_f32", x.data_ptr(), _hip.ptr(weight2d), styles.data_ptr(), _hip.ptr(bias),
+                  y.data_ptr(), n, cin, cout, h, w, clamp, _hip.stream())
+        ctx.clamp = clamp
+        ctx.save_for_backward(x, styles, weight2d, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, styles, w2, y = ctx.saved_tensors
+        n, cin, h, w = x.shape
+        cout = w2.shape[0]
+        gy = gy.contiguous()
+        dx = ds = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _hip.call("smc_torgb_bwd_f32", gy.data_ptr(), y.data_ptr(), w2.data_ptr(), styles.data_ptr(),
+                      dx.data_ptr(), n, cin, cout, h, w, ctx.clamp, 1, 0, _hip.stream())
+        if ctx.needs_input_grad[1]:
+            dxs = torch.empty_like(x)
+            _hip.call("smc_torgb_bwd_f32", gy.data_ptr(), y.data_ptr(), w2.data_ptr(), styles.data_ptr(),
+                      dxs.data_ptr(), n, cin, cout, h, w, ctx.clamp, 0, 0, _hip.stream())
+            ds = torch.empty(n, cin, device=x.device, dtype=torch.float32)
+            _hip.call("smc_channel_dot_f32", dxs.data_ptr(), x.data_ptr(), None, ds.data_ptr(), None, n * cin, h * w, 0,
+                      _hip.stream())
+        return dx, ds, None, None, None
+
+
+def modulated_conv2d(x, weight, styles, noise=None, up=1, down=1, padding=0, resample_filter=None, demodulate=True,
+                     flip_weight=True, fused_modconv=True, spec=None):
+    """[upstream] modulated_conv2d signature, without bias/activation (gain 1, linear, no clamp).
+
+    ``fused_modconv`` is accepted for signature compatibility; both forms compute the same function.
+    Only the synthesis-network shapes are supported: 3x3 (up 1 or 2, padding 1, flip_weight = (up == 1))
+    and 1x1 (up 1, padding 0).
+    """
+    if down != 1:
+        raise NotImplementedError("modulated_conv2d: down > 1 is not on the synthesis path")
+    k = weight.shape[-1]
+    if k == 1 and up == 1 and not demodulate and noise is None and weight.shape[0] <= 4:
+        return ToRGBFn.apply(x, styles, weight[:, :, 0, 0].detach().float().contiguous(), None, -1.0)
+    if padding != k // 2 or flip_weight != (up == 1):
+        raise NotImplementedError("modulated_conv2d: only padding=k//2 with flip_weight=(up==1) is supported")
+    if spec is None:
+        spec = LayerSpec(weight, None, up, resample_filter, demodulate=demodulate, act="linear")
+    if noise is not None:
+        strength = torch.ones([], device=x.device, dtype=torch.float32)
+    else:
+        strength = None
+    return ModConvFn.apply(x, styles, spec, noise, strength, 1.0, -1.0)

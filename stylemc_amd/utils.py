@@ -1,0 +1,122 @@
+"""S-space synthesis driver -- drop-in for the reference's utils.py hot-path helpers.
+
+  block_forward   (utils.py:13-53)   per-block forward from S codes; widths trimmed by `shapes`
+  generate_image  (utils.py:161-216) block loop up to `until_k`; `device` is optional here (the
+                                     reference's find_direction.py:309,312 omits it -> TypeError there)
+  get_temp_shapes (utils.py:100-120) style widths per block; replaces each affine by Identity
+  split_ws        (utils.py:77-87), get_styles (utils.py:123-158), get_mean_std (utils.py:90-97),
+  num_range       (utils.py:64-74)
+The feature-blending branches of generate_image (use_blending, cv2 masks) are out of scope
+ and raise NotImplementedError.
+"""
+import re
+
+import torch
+
+from .torch_utils.ops import upfirdn2d
+
+N_STYLE_CHANNELS = 26
+S_TRAINABLE_SPACE_CHANNELS = [2, 3, 5, 6, 8, 9, 11, 12]
+S_NON_TRAINABLE_SPACE_CHANNELS = [0, 1, 4, 7, 10, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25]
+
+
+def block_forward(self, x, img, ws, shapes, force_fp32=False, fused_modconv=None, **layer_kwargs):
+    assert ws.ndim == 3 and ws.shape[1] == self.num_conv + self.num_torgb and ws.shape[2] == self.w_dim
+    w_iter = iter(ws.unbind(dim=1))
+    if fused_modconv is None:
+        fused_modconv = not self.training
+    if self.in_channels == 0:
+        x = self.const.to(torch.float32).unsqueeze(0).repeat([ws.shape[0], 1, 1, 1])
+        x = self.conv1(x, next(w_iter)[..., :shapes[0]], fused_modconv=fused_modconv, **layer_kwargs)
+    else:
+        assert x.shape[1:] == (self.in_channels, self.resolution // 2, self.resolution // 2)
+        x = x.to(torch.float32)
+        x = self.conv0(x, next(w_iter)[..., :shapes[0]], fused_modconv=fused_modconv, **layer_kwargs)
+        x = self.conv1(x, next(w_iter)[..., :shapes[1]], fused_modconv=fused_modconv, **layer_kwargs)
+    if img is not None:
+        assert img.shape[1:] == (self.img_channels, self.resolution // 2, self.resolution // 2)
+        img = upfirdn2d.upsample2d(img, self.resample_filter)
+    if self.is_last or self.architecture == "skip":
+        y = self.torgb(x, next(w_iter)[..., :shapes[2]], fused_modconv=fused_modconv)
+        y = y.to(dtype=torch.float32, memory_format=torch.contiguous_format)
+        img = img.add_(y) if img is not None else y
+    return x, img
+
+
+def generate_image(G, until_k, styles, temp_shapes, noise_mode="const", device=None, use_blending=False,
+                   xs_original=None, masks_dict=None):
+    if use_blending or xs_original is not None:
+        raise NotImplementedError("feature blending (deeplab masks) is outside the find_direction hot path")
+    x = img = None
+    xs = []
+    row = 0
+    for k, res in enumerate(G.synthesis.block_resolutions):
+        if k > until_k:
+            continue
+        block = getattr(G.synthesis, f"b{res}")
+        width = 2 if res == 4 else 3
+        x, img = block_forward(block, x, img, styles[:, row:row + width, :], temp_shapes[k], noise_mode=noise_mode)
+        row += width
+        xs.append(x)
+    return xs, img
+
+
+def get_temp_shapes(G):
+    shapes = []
+    for res in G.synthesis.block_resolutions:
+        block = getattr(G.synthesis, f"b{res}")
+        if res == 4:
+            width = block.conv1.affine.weight.shape[0]
+            shapes.append((width, width, block.torgb.affine.weight.shape[0]))
+            block.conv1.affine = torch.nn.Identity()
+        else:
+            shapes.append((block.conv0.affine.weight.shape[0], block.conv1.affine.weight.shape[0],
+                           block.torgb.affine.weight.shape[0]))
+            block.conv0.affine = torch.nn.Identity()
+            block.conv1.affine = torch.nn.Identity()
+        block.torgb.affine = torch.nn.Identity()
+    return shapes
+
+
+def split_ws(G, ws):
+    out = []
+    idx = 0
+    ws = ws.to(torch.float32)
+    for res in G.synthesis.block_resolutions:
+        block = getattr(G.synthesis, f"b{res}")
+        out.append(ws.narrow(1, idx, block.num_conv + block.num_torgb))
+        idx += block.num_conv
+    return out
+
+
+@torch.no_grad()
+def get_styles(G, ws, block_ws=None, device=None):
+    """W [n, num_ws, 512] -> packed S [n, 26, 512] (zero padded) + temp shapes; mutates G (affines -> Identity)."""
+    if block_ws is None:
+        block_ws = split_ws(G, ws)
+    styles = torch.zeros(ws.size(0), N_STYLE_CHANNELS, 512, device=device or ws.device)
+    row = 0
+    shapes = []
+    for res, cur in zip(G.synthesis.block_resolutions, block_ws):
+        block = getattr(G.synthesis, f"b{res}")
+        layers = [block.conv1, block.torgb] if res == 4 else [block.conv0, block.conv1, block.torgb]
+        widths = [l.affine.weight.shape[0] for l in layers]
+        shapes.append((widths[0], widths[0], widths[1]) if res == 4 else tuple(widths))
+        for j, layer in enumerate(layers):
+            styles[:, row + j, :widths[j]] = layer.affine(cur[:, j, :])
+            layer.affine = torch.nn.Identity()
+        row += len(layers)
+    return styles, shapes
+
+
+def get_mean_std(device):
+    mean = torch.as_tensor((0.48145466, 0.4578275, 0.40821073), dtype=torch.float, device=device).view(-1, 1, 1)
+    std = torch.as_tensor((0.26862954, 0.26130258, 0.27577711), dtype=torch.float, device=device).view(-1, 1, 1)
+    return mean, std
+
+
+def num_range(s):
+    m = re.match(r"^(\d+)-(\d+)$", s)
+    if m:
+        return list(range(int(m.group(1)), int(m.group(2)) + 1))
+    return [int(v) for v in s.split(",")]

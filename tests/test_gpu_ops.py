@@ -1,0 +1,251 @@
+"""Parity of the HIP kernels (through the C ABI) against golden vectors and the CPU oracle.
+
+Tolerances (fp32, different summation order than the reference's CPU path):
+  elementwise ops: rtol 1e-5; FIR: atol 1e-5 relative to max|y|; modconv forward 2e-5 and backward
+  1e-4 of the tensor's max magnitude; whole-network image 1e-4, style gradients 1e-3 (relative to
+  max |grad|).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def t(a, dev="cpu"):
+    return torch.from_numpy(np.asarray(a)).to(dev)
+
+
+def close(a, b, tol, what=""):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu() if torch.is_tensor(b) else torch.from_numpy(np.asarray(b)).double()
+    scale = max(b.abs().max().item(), 1e-12)
+    err = (a - b).abs().max().item()
+    assert err <= tol * scale, f"{what}: max err {err:.3e} > {tol:.1e} * {scale:.3e}"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from stylemc_amd import build
+    build.build(verbose=False)
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+
+
+ACTS = ["linear", "relu", "lrelu", "tanh", "sigmoid", "elu", "selu", "softplus", "swish"]
+
+
+@pytest.mark.parametrize("act", ACTS)
+@pytest.mark.parametrize("clamp", [None, 0.7])
+def test_bias_act_golden(golden, act, clamp):
+    from stylemc_amd.torch_utils.ops import bias_act
+    g = golden("ops_bias_act.npz")
+    name = f"{act}_c{'none' if clamp is None else clamp}"
+    x = t(g[f"{name}/x"], DEV).requires_grad_(True)
+    b = t(g[f"{name}/b"], DEV).requires_grad_(True)
+    y = bias_act.bias_act(x, b, act=act, clamp=clamp)
+    close(y, g[f"{name}/y"], 1e-5, f"{name} y")
+    dx, db = torch.autograd.grad(y, [x, b], t(g[f"{name}/dy"], DEV))
+    close(dx, g[f"{name}/dx"], 1e-5, f"{name} dx")
+    close(db, g[f"{name}/db"], 1e-5, f"{name} db")
+
+
+def test_bias_act_second_order_and_dim():
+    from oracle import ops as O
+    from stylemc_amd.torch_utils.ops import bias_act
+    gen = torch.Generator().manual_seed(0)
+    for act in ("tanh", "sigmoid", "elu", "selu", "softplus", "swish"):
+        x0 = torch.randn(2, 3, 5, 7, generator=gen)
+        b0 = torch.randn(3, generator=gen)
+        outs = []
+        for dev, fn in ((DEV, bias_act.bias_act), ("cpu", O.bias_act)):
+            x = x0.to(dev).requires_grad_(True)
+            b = b0.to(dev).requires_grad_(True)
+            y = fn(x, b, act=act)
+            (gx,) = torch.autograd.grad(y.square().sum(), x, create_graph=True)
+            (ggx,) = torch.autograd.grad(gx.sum(), x)
+            outs.append((y, gx, ggx))
+        for a, r, nm in zip(outs[0], outs[1], ("y", "dx", "ddx")):
+            close(a, r, 2e-5, f"{act} {nm}")
+    x = torch.randn(6, 9, generator=gen)
+    b = torch.randn(6, generator=gen)
+    close(bias_act.bias_act(x.to(DEV), b.to(DEV), dim=0, act="lrelu", alpha=0.1, gain=3.0, clamp=2.0),
+          O.bias_act(x, b, dim=0, act="lrelu", alpha=0.1, gain=3.0, clamp=2.0), 1e-6, "dim0")
+    # odd sizes exercise the scalar path
+    x = torch.randn(3, 5, 3, 3, generator=gen)
+    close(bias_act.bias_act(x.to(DEV), b[:5].to(DEV), act="lrelu", clamp=0.5),
+          O.bias_act(x, b[:5], act="lrelu", clamp=0.5), 1e-6, "odd")
+
+
+UFD = ["blur_conv0", "up2_img", "down2_adj", "blur_adj", "rect_up2_down1", "crop_neg_pad", "odd_filter",
+       "sep_filter8", "up4_down3", "single_pixel"]
+
+
+@pytest.mark.parametrize("case", UFD)
+def test_upfirdn2d_golden(golden, case):
+    from stylemc_amd.torch_utils.ops import upfirdn2d
+    g = golden("ops_upfirdn2d.npz")
+    p = lambda k: g[f"{case}/{k}"]
+    x = t(p("x"), DEV).requires_grad_(True)
+    y = upfirdn2d.upfirdn2d(x, t(p("f"), DEV), up=[int(v) for v in p("up")], down=[int(v) for v in p("down")],
+                            padding=[int(v) for v in p("pad")], flip_filter=bool(p("flip")), gain=float(p("gain")))
+    close(y, p("y"), 1e-5, f"{case} y")
+    (dx,) = torch.autograd.grad(y, x, t(p("dy"), DEV))
+    close(dx, p("dx"), 1e-5, f"{case} dx")
+
+
+@pytest.mark.parametrize("shape,up,down,pad,flip", [
+    ((2, 3, 256, 256), 2, 1, [2, 1, 2, 1], False),     # img upsample at 512
+    ((1, 64, 129, 129), 1, 1, [1, 1, 1, 1], False),    # conv0 blur
+    ((1, 64, 128, 128), 1, 1, [2, 2, 2, 2], True),     # blur adjoint
+    ((2, 3, 512, 512), 1, 2, [1, 2, 1, 2], True),      # upsample adjoint
+    ((1, 2, 37, 300), 3, 2, [5, -2, 0, 3], False),     # ragged generic
+])
+def test_upfirdn2d_vs_oracle_large(shape, up, down, pad, flip):
+    from oracle import ops as O
+    from stylemc_amd.torch_utils.ops import upfirdn2d
+    gen = torch.Generator().manual_seed(1)
+    x = torch.randn(shape, generator=gen)
+    f = O.setup_filter([1, 3, 3, 1])
+    ref = O.upfirdn2d(x, f, up=up, down=down, padding=pad, flip_filter=flip, gain=4)
+    out = upfirdn2d.upfirdn2d(x.to(DEV), f.to(DEV), up=up, down=down, padding=pad, flip_filter=flip, gain=4)
+    close(out, ref, 1e-5, "upfirdn2d large")
+
+
+def _pair_layers(cin, cout, res, up, clamp, seed=0, kind="conv"):
+    from oracle import networks as ON
+    from stylemc_amd import networks as PN
+    if kind == "conv":
+        o = ON.SynthesisLayer(cin, cout, 512, res, up=up, conv_clamp=clamp)
+        p = PN.SynthesisLayer(cin, cout, 512, res, up=up, conv_clamp=clamp)
+    else:
+        o = ON.ToRGBLayer(cin, 3, 512, conv_clamp=clamp)
+        p = PN.ToRGBLayer(cin, 3, 512, conv_clamp=clamp)
+    gen = torch.Generator().manual_seed(seed)
+    sd = {}
+    for k, v in o.state_dict().items():
+        if k.endswith("resample_filter"):
+            sd[k] = v
+        elif k.endswith("noise_strength") or k.endswith("bias"):
+            sd[k] = torch.randn(v.shape, generator=gen) * 0.3
+        else:
+            sd[k] = torch.randn(v.shape, generator=gen)
+    o.load_state_dict(sd)
+    p.load_state_dict(sd)
+    o.affine = torch.nn.Identity()
+    p.affine = torch.nn.Identity()
+    return o.eval(), p.to(DEV).eval()
+
+
+@pytest.mark.parametrize("cin,cout,res,up,n", [
+    (32, 32, 16, 1, 2), (64, 32, 32, 2, 2), (512, 512, 4, 1, 3), (512, 512, 8, 2, 2), (128, 64, 64, 1, 1),
+    (256, 128, 32, 2, 1), (512, 256, 16, 2, 4),
+])
+@pytest.mark.parametrize("noise_mode", ["const", "none"])
+def test_synthesis_layer_vs_oracle(cin, cout, res, up, n, noise_mode):
+    o, p = _pair_layers(cin, cout, res, up, clamp=1.0 if cin == 32 else 256.0)
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(n, cin, res // up, res // up, generator=gen)
+    s = torch.randn(n, cin, generator=gen) * 0.5 + 1
+    cot = torch.randn(n, cout, res, res, generator=gen)
+    xr, sr = x.clone().requires_grad_(True), s.clone().requires_grad_(True)
+    yr = o(xr, sr, noise_mode=noise_mode, fused_modconv=True)
+    dxr, dsr = torch.autograd.grad((yr * cot).sum(), [xr, sr])
+    xg, sg = x.to(DEV).requires_grad_(True), s.to(DEV).requires_grad_(True)
+    yg = p(xg, sg, noise_mode=noise_mode)
+    dxg, dsg = torch.autograd.grad((yg * cot.to(DEV)).sum(), [xg, sg])
+    close(yg, yr, 2e-5, "y")
+    close(dxg, dxr, 1e-4, "dx")
+    close(dsg, dsr, 1e-4, "ds")
+
+
+def test_synthesis_layer_grad_subsets():
+    """needs_input_grad pruning: styles-only and x-only backward give the same numbers."""
+    o, p = _pair_layers(64, 64, 16, 2, clamp=256.0)
+    gen = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 64, 8, 8, generator=gen).to(DEV)
+    s = (torch.randn(2, 64, generator=gen) * 0.5 + 1).to(DEV)
+    cot = torch.randn(2, 64, 16, 16, generator=gen).to(DEV)
+    xa, sa = x.clone().requires_grad_(True), s.clone().requires_grad_(True)
+    dxa, dsa = torch.autograd.grad((p(xa, sa, noise_mode="const") * cot).sum(), [xa, sa])
+    sb = s.clone().requires_grad_(True)
+    (dsb,) = torch.autograd.grad((p(x, sb, noise_mode="const") * cot).sum(), [sb])
+    xc = x.clone().requires_grad_(True)
+    (dxc,) = torch.autograd.grad((p(xc, s, noise_mode="const") * cot).sum(), [xc])
+    close(dsb, dsa, 1e-6, "ds only")
+    close(dxc, dxa, 1e-6, "dx only")
+
+
+@pytest.mark.parametrize("cin,res,n,clamp", [(512, 4, 2, 256.0), (64, 64, 3, 0.3), (32, 128, 1, None), (128, 9, 2, 1.0)])
+def test_torgb_vs_oracle(cin, res, n, clamp):
+    o, p = _pair_layers(cin, 3, res, 1, clamp=clamp, kind="rgb")
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(n, cin, res, res, generator=gen)
+    s = torch.randn(n, cin, generator=gen) * 0.5 + 1
+    cot = torch.randn(n, 3, res, res, generator=gen)
+    xr, sr = x.clone().requires_grad_(True), s.clone().requires_grad_(True)
+    yr = o(xr, sr)
+    dxr, dsr = torch.autograd.grad((yr * cot).sum(), [xr, sr])
+    xg, sg = x.to(DEV).requires_grad_(True), s.to(DEV).requires_grad_(True)
+    yg = p(xg, sg)
+    dxg, dsg = torch.autograd.grad((yg * cot.to(DEV)).sum(), [xg, sg])
+    close(yg, yr, 2e-5, "y")
+    close(dxg, dxr, 2e-5, "dx")
+    close(dsg, dsr, 1e-4, "ds")
+
+
+def _product_G(res, cbase, clamp, seed=7):
+    from stylemc_amd import networks, synthetic
+    cfg = synthetic.generator_config(resolution=res, channel_base=cbase, conv_clamp=clamp)
+    return networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=seed), device=DEV)
+
+
+@pytest.mark.parametrize("tag", ["r32", "r16_clamp"])
+def test_synthesis_tiny_golden(golden, tag):
+    """Whole S-space synthesis fwd + style gradients vs vectors from the reference's own driver."""
+    from stylemc_amd import utils
+    g = golden("synthesis_tiny.npz")
+    res, cbase, n, until_k = [int(v) for v in g[f"{tag}/meta"]]
+    G = _product_G(res, cbase, float(g[f"{tag}/clamp"]))
+    shapes = utils.get_temp_shapes(G)
+    styles = t(g[f"{tag}/styles"], DEV).requires_grad_(True)
+    xs, img = utils.generate_image(G, until_k, styles, shapes, "const")
+    for k, xk in enumerate(xs):
+        close(xk, g[f"{tag}/xs{k}"], 1e-4, f"xs{k}")
+    close(img, g[f"{tag}/img"], 1e-4, "img")
+    (ds,) = torch.autograd.grad((img * t(g[f"{tag}/cot"], DEV)).sum(), styles)
+    close(ds, g[f"{tag}/dstyles"], 1e-3, "dstyles")
+
+
+def test_synthesis_1024_vs_oracle():
+    """FFHQ-1024 config-f geometry, N=1: full forward image + direction-row gradients vs the CPU oracle."""
+    from oracle import networks as ON
+    from oracle import synthesis as OS
+    from stylemc_amd import synthetic, utils
+    cfg = synthetic.generator_config(resolution=1024)
+    sd = synthetic.generator_state_dict(cfg, seed=0)
+    G = _product_G(1024, 32768, 256.0, seed=0)
+    Go = torch.nn.Module()
+    Go.synthesis = ON.SynthesisNetwork(512, 1024, 3, channel_base=32768, conv_clamp=256.0)
+    Go.synthesis.load_state_dict({k[10:]: v for k, v in sd.items() if k.startswith("synthesis.")}, strict=False)
+    Go.eval().requires_grad_(False)
+    shapes_p, shapes_o = utils.get_temp_shapes(G), OS.get_temp_shapes(Go)
+    assert shapes_p == shapes_o
+    styles = synthetic.synthetic_styles(1, seed=0)
+    gen = torch.Generator().manual_seed(2)
+    cot = torch.randn(1, 3, 1024, 1024, generator=gen)
+    so = styles.clone().requires_grad_(True)
+    _, img_o = OS.generate_image(Go, 8, so, shapes_o, "const")
+    (ds_o,) = torch.autograd.grad((img_o * cot).sum(), so)
+    sp = styles.to(DEV).requires_grad_(True)
+    _, img_p = utils.generate_image(G, 8, sp, shapes_p, "const")
+    (ds_p,) = torch.autograd.grad((img_p * cot.to(DEV)).sum(), sp)
+    close(img_p, img_o, 1e-4, "img 1024")
+    T = utils.S_TRAINABLE_SPACE_CHANNELS
+    close(ds_p[:, T], ds_o[:, T], 2e-3, "dstyles trainable rows")
+    cos = torch.nn.functional.cosine_similarity(ds_p.cpu().double().flatten(), ds_o.double().flatten(), dim=0)
+    assert cos > 0.9999, cos
