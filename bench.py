@@ -1,0 +1,189 @@
+#!/usr/bin/env python
+"""find_direction throughput on MI355X (BASELINE.json metric), one JSON line on rank 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one find_direction iteration (find_direction.py:292-347) on synthetic inputs that are
+resident in HBM before timing: a config-f FFHQ-1024 generator with seeded weights, S codes
+[129, 26, 512] ~ N(1, 0.5), seeded CLIP ViT-B/32 + IR-SE50, --clip_type small, landmarks 0.
+Each GPU processes a batch of 4 seeds per step (weak scaling: global batch = 4 x N, one RCCL
+all_reduce of the direction gradient per step).  value = images/s = 2 x seeds/s (edited + original
+image per seed), seeds counted exactly (the batch picker can draw the short
+last batch of the 129 seeds).
+
+roofline: the dominant kernel family, ``conv_gemm_kernel`` (the MFMA implicit-GEMM modulated conv,
+all template instantiations): algorithmic FLOPs of each launch (dense MACs x 2 of the conv it
+computes) / its duration, timed with HIP events around every launch in the
+timed region, against the fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).  traffic: HBM
+bytes per launch from the rocprofv3 PMC pass recorded in profiles/pmc_traffic.json (null if absent).
+
+cpu_baseline (rank 0, N=1): the test oracle (pure-torch fp32 CPU restatement of the reference
+algorithm, oracle/) running the same step at FFHQ-1024 with batch 1 for --cpu-iters iterations on
+--cpu-threads host threads.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3
+METRIC = "find_direction images/sec @ FFHQ-1024 bs=4, 1/2/4/8 GPU; dir cosine-sim vs ref"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--resolution", type=int, default=1024)
+    p.add_argument("--batch", type=int, default=4, help="seeds per GPU per step")
+    p.add_argument("--n-seeds", type=int, default=129)
+    p.add_argument("--clip-type", default="small")
+    p.add_argument("--cpu-iters", type=int, default=4)
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-kernel-timer", action="store_true", help="skip the per-launch HIP events")
+    return p.parse_args()
+
+
+def cpu_baseline(resolution, iters, threads):
+    """Oracle find_direction on the host: `iters` iterations, batch 1 (TEST ORACLE used as the baseline)."""
+    from oracle import find_direction as OF
+    from oracle import losses as OL
+    from oracle import networks as ON
+    from oracle import synthesis as OS
+    from stylemc_amd import synthetic
+    from stylemc_amd.find_direction import initial_delta
+    torch.set_num_threads(threads)
+    cfg = synthetic.generator_config(resolution=resolution)
+    sd = synthetic.generator_state_dict(cfg, seed=0)
+    G = torch.nn.Module()
+    G.synthesis = ON.SynthesisNetwork(512, resolution, 3, channel_base=cfg["channel_base"], conv_clamp=256.0)
+    G.synthesis.load_state_dict({k[10:]: v for k, v in sd.items() if k.startswith("synthesis.")}, strict=False)
+    G.eval().requires_grad_(False)
+    shapes = OS.get_temp_shapes(G)
+    vis = OL.CLIPVisual().eval()
+    vis.load_state_dict(synthetic.seeded_state_dict(vis, seed=4))
+    vis.requires_grad_(False)
+    clip = OL.CLIPLoss(vis, synthetic.text_direction("a photo of a face of a feminine woman with no makeup",
+                                                     "a photo of a face of a masculine man"))
+    net = OL.IRSE50().eval()
+    net.load_state_dict(synthetic.seeded_state_dict(net, seed=3))
+    net.requires_grad_(False)
+    styles = synthetic.synthetic_styles(iters, seed=0)
+    t0 = time.perf_counter()
+    OF.find_direction(G, styles, clip, OL.IDLoss(net), shapes, int(resolution).bit_length() - 3, batch_size=1,
+                      n_epochs=1, max_iterations=iters, init_delta=initial_delta(0, 0.01))
+    dt = time.perf_counter() - t0
+    return {"value": 2 * iters / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{iters} find_direction iterations x 1 seed (FFHQ-{resolution}, CLIP ViT-B/32 + IR-SE50) "
+                      f"in {dt:.1f} s, oracle/ pure-torch fp32 CPU restatement, {threads} threads"}
+
+
+def pmc_traffic():
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("conv_gemm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    from stylemc_amd import _hip, build
+    from stylemc_amd import dist as sdist
+    world = sdist.init_from_env(use_cuda=True)
+    dev = torch.device("cuda", world.local_rank)
+    torch.cuda.set_device(dev)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    if world.rank == 0:
+        build.build(verbose=False)
+    world.barrier()
+    _hip.load()
+
+    from stylemc_amd.find_direction import DirectionFinder, build_clip_losses, initial_delta, load_generator
+    from stylemc_amd.id_loss import IDLoss
+    from stylemc_amd import synthetic
+
+    G = load_generator("synthetic", args.resolution, dev)
+    styles = synthetic.synthetic_styles(args.n_seeds, seed=0).to(dev)
+    clip = build_clip_losses(args.clip_type, dev, "a photo of a face of a feminine woman with no makeup",
+                             "a photo of a face of a masculine man")
+    finder = DirectionFinder(G, styles, clip, IDLoss("a", device=dev, weights=None), resolution=args.resolution,
+                             batch_size=args.batch, global_batch=args.batch * world.world_size, seed=0, world=world,
+                             init_delta=initial_delta(0, 0.01), n_epochs=1000)
+    for _ in range(args.warmup):
+        finder.step()
+    torch.cuda.synchronize()
+    world.barrier()
+
+    timer = None if args.no_kernel_timer else _hip.KernelTimer("conv_gemm")
+    _hip.set_timer(timer)
+    seeds = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        last = finder.step()
+        lo = last["batch"] * finder.B
+        seeds += min(lo + finder.B, finder.n_items) - lo
+    torch.cuda.synchronize()
+    world.barrier()
+    dt = time.perf_counter() - t0
+    _hip.set_timer(None)
+    dt = world.all_max(dt, dev)
+    finite = bool(torch.isfinite(finder.delta).all().item())
+
+    roofline = None
+    if timer is not None:
+        s = timer.summary()
+        achieved = s["flops"] / s["seconds"] / 1e12 if s["seconds"] > 0 else 0.0
+        roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),
+                    "kernel": "conv_gemm_kernel (all instantiations)", "launches": s["launches"],
+                    "avg_launch_us": round(1e6 * s["seconds"] / max(s["launches"], 1), 2),
+                    "alg_gflop_per_launch": round(s["flops"] / max(s["launches"], 1) / 1e9, 3),
+                    "share_of_step_time": round(s["seconds"] / dt, 4)}
+
+    if world.rank != 0:
+        return
+    out = {
+        "metric": METRIC,
+        "value": round(2 * seeds / dt, 3),
+        "unit": "images/s",
+        "n_gpus": world.world_size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * dt / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded config-f weights, S ~ N(1, 0.5) for 129 seeds, seeded CLIP/IR-SE50)",
+        "config": {"workload": "find_direction step: 2x StyleGAN2 S-space synthesis fwd + 1 bwd (HIP), "
+                               "CLIP ViT-B/32 + IR-SE50 fwd/bwd (PyTorch-ROCm), SGD",
+                   "resolution": args.resolution, "batch_per_gpu": args.batch,
+                   "global_batch": args.batch * world.world_size, "seeds_per_sec": round(seeds / dt, 3),
+                   "parallelism": f"dp{world.world_size}", "clip_type": args.clip_type, "landmarks_loss_coef": 0,
+                   "direction_finite": finite},
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if world.world_size == 1 and not args.no_cpu_baseline:
+        threads = min(args.cpu_threads, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(args.resolution, args.cpu_iters, threads)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -9,6 +9,9 @@ shipped script cannot run: generate_image is called without ``device``, find_dir
   * two syntheses (edited, original), compute_loss, backward, SGD p -= lr_t * g      (:309-339)
   * the returned direction is ``styles_direction`` as the reference saves it (:349-351): the delta
     written into it at the start of the LAST iteration (the final SGD step is not copied back).
+  * ``init_delta``: the reference starts from exactly zero, where img == original and the directional
+    CLIP term normalises a zero vector (clip_loss.py:29-30 -> NaN); runs start from a seeded small
+    direction instead (stylemc_amd.find_direction.initial_delta).
 """
 import math
 
@@ -25,7 +28,7 @@ def cosine_lr(lr0, it, total):
 
 def find_direction(G, styles_array, clip_loss, id_loss, temp_shapes, until_k, batch_size=4, learning_rate=1.5,
                    n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
-                   seed=0, max_iterations=None, log=None):
+                   seed=0, max_iterations=None, log=None, init_delta=None):
     T = S_TRAINABLE_SPACE_CHANNELS
     rng = np.random.RandomState(seed)
     mean, std = get_mean_std()
@@ -33,7 +36,10 @@ def find_direction(G, styles_array, clip_loss, id_loss, temp_shapes, until_k, ba
     num_batches = math.ceil(n_items / batch_size)
     total = num_batches * n_epochs
     styles_direction = torch.zeros(1, N_STYLE_CHANNELS, 512)
-    delta = styles_direction[:, T].clone().requires_grad_(True)
+    delta = styles_direction[:, T].clone()
+    if init_delta is not None:  # see stylemc_amd.find_direction.initial_delta: zero start is 0/0 in CLIP
+        delta = init_delta.detach().clone().reshape(1, len(T), 512).float()
+    delta.requires_grad_(True)
     it = 0
     for _ in range(n_epochs):
         for _ in range(num_batches):
@@ -54,8 +60,8 @@ def find_direction(G, styles_array, clip_loss, id_loss, temp_shapes, until_k, ba
             with torch.no_grad():
                 delta.add_(delta.grad, alpha=-lr_t)
             if log is not None:
-                log.append({"it": it, "batch": i, "lr": lr_t, "loss": float(loss),
-                            "grad_norm": float(delta.grad.norm()), **{k: float(v) for k, v in parts.items()}})
+                log.append({"it": it, "batch": i, "lr": lr_t, "loss": float(loss.detach()),
+                            "grad_norm": float(delta.grad.norm()), **{k: float(torch.as_tensor(v).detach()) for k, v in parts.items()}})
             if max_iterations is not None and it >= max_iterations:
                 return styles_direction, delta.detach()
     return styles_direction, delta.detach()

@@ -1,0 +1,39 @@
+"""Directional CLIP loss (clip_loss.py:7-34): mean(1 - cos(norm(E(tgt) - E(src)), norm(T+ - T-))).
+
+Without the third-party ``clip`` package and its weights (absent offline) the text direction is either
+given (``text_features``) or a seeded unit vector derived from the two prompts
+(``synthetic.text_direction``); the image tower is ``clip_model.VisionTransformer``.
+``per_sample`` returns 1 - cos_i so the loss can be sharded over ranks and summed.
+"""
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import clip_model, synthetic
+
+
+class CLIPLoss(nn.Module):
+    def __init__(self, device="cuda", text_prompt="", negative_text_prompt="", clip_type="small", visual=None,
+                 text_features=None, visual_state_dict=None, seed=4):
+        super().__init__()
+        name = "ViT-B/32" if clip_type == "small" else "ViT-B/16"
+        self.model_name = name
+        self.visual = visual if visual is not None else clip_model.build_visual(name, visual_state_dict, seed=seed,
+                                                                                device=device)
+        if text_features is None:
+            text_features = synthetic.text_direction(text_prompt, negative_text_prompt)
+        t = torch.as_tensor(text_features, dtype=torch.float32).reshape(1, -1).to(device)
+        self.register_buffer("text_features", t / t.norm(dim=1, keepdim=True))
+
+    def encode_image(self, image):
+        return self.visual(image)
+
+    def per_sample(self, src_image, tgt_image):
+        with torch.no_grad():
+            src = self.visual(src_image)
+        f = self.visual(tgt_image) - src
+        f = f / f.norm(dim=1, keepdim=True)
+        return 1 - F.cosine_similarity(f, self.text_features)
+
+    def forward(self, src_image, tgt_image):
+        return self.per_sample(src_image, tgt_image).mean()

@@ -1,0 +1,257 @@
+"""find_direction on MI355X: drop-in for the reference's find_direction.py (CLI flags kept).
+
+The optimisation (find_direction.py:259-351) is restated with its intended behaviour:
+  * lr_t = 0.5*lr0*(1 + cos(pi*t/T)), T = n_epochs*ceil(n/B)                        (:297-301)
+  * batch index i = randint(0, ceil(n/B)) with replacement (seeded here; unseeded in :303)
+  * styles2 = styles + direction on rows T = [2,3,5,6,8,9,11,12]                  (:307-308)
+  * loss = id_c*ID(img, orig) + clip_c*CLIP(orig, img) + l2_c*mse(styles2[:,T], styles[:,T])  (:172-200)
+  * SGD p -= lr_t * grad                                                             (:336-339)
+  * output npz key 's' [1,26,512]: ``styles_direction`` as the reference saves it -- the delta written
+    into it at the start of the last iteration (:307, :349-351)
+Start point: the reference starts from delta = 0 (:270-273), where img == original_img bit for bit and
+the directional CLIP loss normalises a zero feature difference (clip_loss.py:29-30): 0/0 = NaN, which
+then poisons every later step.  Runs therefore start from ``initial_delta(seed, init_std)``, a seeded
+N(0, init_std) direction (--init_std 0 reproduces the literal zero start).
+Landmarks: the reference computes that term under torch.no_grad (:90), so it never changes the
+direction; a non-zero --landmarks_loss_coef is accepted and ignored with a warning.
+generate_image is called with the missing ``device`` fixed (:309,312 raise TypeError as shipped).
+
+Multi-GPU: every rank draws the same i, takes its contiguous slice of the global batch, and one
+all_reduce(SUM) per step combines the gradient and the loss terms (stylemc_amd.dist).
+"""
+import math
+import os
+import time
+import warnings
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import dist as _dist
+from . import utils
+
+N_STYLE_CHANNELS = utils.N_STYLE_CHANNELS
+S_TRAINABLE_SPACE_CHANNELS = utils.S_TRAINABLE_SPACE_CHANNELS
+S_NON_TRAINABLE_SPACE_CHANNELS = utils.S_NON_TRAINABLE_SPACE_CHANNELS
+RESOLUTION_DICT = {256: 6, 512: 7, 1024: 8}
+
+
+def unprocess(img, mean, std, size=224):
+    """find_direction.py:49-52 with torchvision-0.8 tensor Resize(224, BICUBIC) + CenterCrop(224)."""
+    x = (img * 127.5 + 128).clamp(0, 255)
+    h, w = x.shape[-2:]
+    nh, nw = (size, int(size * w / h)) if h <= w else (int(size * h / w), size)
+    x = F.interpolate(x, size=(nh, nw), mode="bicubic", align_corners=False)
+    top, left = int(round((nh - size) / 2.0)), int(round((nw - size) / 2.0))
+    x = x[..., top:top + size, left:left + size]
+    return (x / 255 - mean) / std
+
+
+def initial_delta(seed=0, init_std=0.01, device="cpu"):
+    """Seeded starting direction [1, 8, 512] (see the module docstring: an exact zero start is NaN)."""
+    g = torch.Generator().manual_seed(int(seed) + 7919)
+    return (torch.randn(1, len(S_TRAINABLE_SPACE_CHANNELS), 512, generator=g) * init_std).to(device)
+
+
+def cosine_lr(lr0, it, total):
+    return float(np.cos(np.pi * it / total) * lr0 * 0.5 + lr0 * 0.5)
+
+
+class DirectionFinder:
+    """State of one find_direction run; ``step()`` is one iteration of the reference's hot loop."""
+
+    def __init__(self, G, styles_array, clip_losses, id_loss, resolution=1024, batch_size=4, learning_rate=1.5,
+                 n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
+                 seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None):
+        self.G = G
+        self.device = styles_array.device
+        self.styles_array = styles_array
+        self.clip_losses = clip_losses            # [(CLIPLoss, weight)], 'double' -> [(B/32, 1), (B/16, .5)]
+        self.id_loss = id_loss
+        self.until_k = RESOLUTION_DICT.get(resolution, int(math.log2(resolution)) - 2)
+        self.B = int(global_batch or batch_size)
+        self.lr0 = learning_rate
+        self.n_epochs = n_epochs
+        self.coef = dict(id=identity_loss_coef, l2=l2_reg_coef, clip=clip_loss_coef)
+        self.noise_mode = noise_mode
+        self.world = world or _dist.World()
+        self.temp_shapes = temp_shapes if temp_shapes is not None else utils.get_temp_shapes(G)
+        self.n_items = styles_array.shape[0]
+        self.num_batches = math.ceil(self.n_items / self.B)
+        self.total_iterations = self.num_batches * n_epochs
+        self.rng = np.random.RandomState(seed)
+        self.it = 0
+        T = S_TRAINABLE_SPACE_CHANNELS
+        self.styles_direction = torch.zeros(1, N_STYLE_CHANNELS, 512, device=self.device)
+        self.delta = self.styles_direction[:, T].clone()
+        if init_delta is not None:
+            self.delta = init_delta.detach().to(self.device, torch.float32).reshape(1, len(T), 512).clone()
+        self.mean, self.std = utils.get_mean_std(self.device)
+        self.images_per_step = 2 * self.B          # edited + original per seed
+        self.last = None
+
+    def load_direction(self, direction):
+        """--resume: start from a saved [1, 26, 512] direction (the reference's :266-268, fixed)."""
+        d = torch.as_tensor(direction, dtype=torch.float32, device=self.device).reshape(1, N_STYLE_CHANNELS, 512)
+        self.styles_direction.copy_(d)
+        self.delta = d[:, S_TRAINABLE_SPACE_CHANNELS].clone()
+
+    def _local_terms(self, styles, denom):
+        """Sum-form loss of this rank's shard: every per-sample term / global batch size."""
+        T = S_TRAINABLE_SPACE_CHANNELS
+        d = self.delta.detach().clone().requires_grad_(True)
+        img = utils.generate_image_rows(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+        with torch.no_grad():
+            orig = utils.generate_image_rows(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
+        id_terms = self.id_loss.per_sample(img, orig)
+        src, tgt = unprocess(orig, self.mean, self.std), unprocess(img, self.mean, self.std)
+        clip_terms = sum(w * cl.per_sample(src, tgt) for cl, w in self.clip_losses)
+        sT = styles[:, T]
+        l2_sum = ((sT + d) - sT).square().sum()
+        id_part = self.coef["id"] * id_terms.sum() / denom
+        clip_part = self.coef["clip"] * clip_terms.sum() / denom
+        l2_part = self.coef["l2"] * l2_sum / (denom * len(T) * 512)
+        (g,) = torch.autograd.grad(id_part + clip_part + l2_part, d)
+        return g, torch.stack([clip_part.detach(), id_part.detach(), torch.zeros_like(l2_part), l2_part.detach()])
+
+    def step(self):
+        self.it += 1
+        lr_t = cosine_lr(self.lr0, self.it, self.total_iterations)
+        i = self.rng.randint(0, self.num_batches)
+        lo, hi = i * self.B, min((i + 1) * self.B, self.n_items)
+        a, b = _dist.shard_rows(lo, hi, self.world.rank, self.world.world_size)
+        self.styles_direction[:, S_TRAINABLE_SPACE_CHANNELS] = self.delta
+        buf = torch.zeros(self.delta.numel() + 4, device=self.device)
+        if b > a:
+            g, parts = self._local_terms(self.styles_array[a:b], hi - lo)
+            buf[:-4] = g.flatten()
+            buf[-4:] = parts
+        self.world.all_reduce_(buf)
+        grad = buf[:-4].view_as(self.delta)
+        self.delta = torch.add(self.delta, grad, alpha=-lr_t)  # == torch.optim.SGD step (find_direction.py:339)
+        self.last = {"it": self.it, "batch": i, "lr": lr_t, "grad": grad, "parts": buf[-4:]}
+        return self.last
+
+    def log_line(self):
+        p = self.last["parts"].tolist()
+        g = self.last["grad"].norm().item()
+        return (f"Iteration {self.it}, gradient norm: {g:.4f}, lr {self.last['lr']:.4f}\n"
+                f"Total loss: {sum(p):.4f}, clip loss: {p[0]:.4f}, identity loss: {p[1]:.4f}, "
+                f"landmarks loss: {p[2]:.4f}, l2 loss: {p[3]:.4f}")
+
+    def save(self, path):
+        np.savez(path, s=self.styles_direction.detach().cpu().numpy())
+
+
+# ------------------------------------------------------------------------------------------- CLI helpers
+
+
+def load_generator(network, resolution, device):
+    """'synthetic' -> seeded config-f generator; *.pt/*.pth/*.safetensors -> state_dict (legacy.py:172-203 names)."""
+    from . import networks, synthetic
+    cfg = synthetic.generator_config(resolution=resolution)
+    if network in (None, "", "synthetic"):
+        return networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=device)
+    if network.endswith(".pkl") or network.startswith("http"):
+        raise SystemExit(f"{network}: network pickles execute embedded code on load and cannot be fetched "
+                         f"offline; convert G_ema to a state_dict (.pt) first")
+    if network.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        sd = load_file(network)
+    else:
+        sd = torch.load(network, map_location="cpu", weights_only=True)
+    sd = {k[len("G_ema."):] if k.startswith("G_ema.") else k: v for k, v in sd.items()}
+    return networks.build_generator(cfg, sd, device=device)
+
+
+def load_styles(s_input, n_seeds, device, seed=0):
+    from . import synthetic
+    if s_input:
+        return torch.tensor(np.load(s_input)["s"], device=device, dtype=torch.float32)
+    return synthetic.synthetic_styles(n_seeds, seed=seed).to(device)
+
+
+def build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip_loss_type="default"):
+    from .clip_loss import CLIPLoss
+    if clip_loss_type != "default":
+        raise NotImplementedError("the StyleGAN-NADA losses (clip_loss_nada.py) are outside the hot path")
+    if clip_type == "double":
+        return [(CLIPLoss(device, text_prompt, negative_text_prompt, "small"), 1.0),
+                (CLIPLoss(device, text_prompt, negative_text_prompt, "large"), 0.5)]
+    return [(CLIPLoss(device, text_prompt, negative_text_prompt, clip_type), 1.0)]
+
+
+def _cli():
+    import click
+
+    @click.command()
+    @click.pass_context
+    @click.option("--network", "network_pkl", default="synthetic", help="generator state_dict (.pt/.safetensors) or 'synthetic'")
+    @click.option("--noise-mode", type=click.Choice(["const", "random", "none"]), default="const", show_default=True)
+    @click.option("--s_input", type=str, default=None, metavar="FILE", help="npz with key 's' [n,26,512]")
+    @click.option("--outdir", type=str, required=True, default="runs/male2female_id0.75_clip1.0_lr2.5_power2.0/")
+    @click.option("--text_prompt", type=str, required=True, default="a photo of a face of a feminine woman with no makeup")
+    @click.option("--negative_text_prompt", type=str, default="a photo of a face of a masculine man")
+    @click.option("--clip_type", type=str, default="double")
+    @click.option("--clip_loss_type", type=str, default="default")
+    @click.option("--resolution", type=int, default=256)
+    @click.option("--batch_size", type=int, default=4)
+    @click.option("--learning_rate", type=float, default=1.5)
+    @click.option("--n_epochs", type=int, default=4)
+    @click.option("--resume", type=str, default=None)
+    @click.option("--identity_loss_coef", type=float, default=0.6)
+    @click.option("--landmarks_loss_coef", type=float, default=25.0)
+    @click.option("--l2_reg_coef", type=float, default=0.1)
+    @click.option("--clip_loss_coef", type=float, default=1.0)
+    @click.option("--n_seeds", type=int, default=129, help="rows of synthetic S when --s_input is absent")
+    @click.option("--seed", type=int, default=0, help="seed of the batch picker (unseeded in the reference)")
+    @click.option("--per_gpu_batch", is_flag=True, help="throughput mode: global batch = batch_size x world")
+    @click.option("--max_iterations", type=int, default=None)
+    @click.option("--init_std", type=float, default=0.01, help="std of the seeded start direction (0 = reference)")
+    def find_direction(ctx, network_pkl, noise_mode, s_input, outdir, text_prompt, negative_text_prompt, clip_type,
+                       clip_loss_type, resolution, batch_size, learning_rate, n_epochs, resume, identity_loss_coef,
+                       landmarks_loss_coef, l2_reg_coef, clip_loss_coef, n_seeds, seed, per_gpu_batch, max_iterations,
+                       init_std):
+        from .id_loss import IDLoss
+        world = _dist.init_from_env(use_cuda=True)
+        device = torch.device("cuda", world.local_rank)
+        torch.cuda.set_device(device)
+        if landmarks_loss_coef != 0:
+            warnings.warn("landmarks loss adds no gradient in the reference (no_grad, find_direction.py:90); ignored")
+        G = load_generator(network_pkl, resolution if network_pkl == "synthetic" else 1024, device)
+        os.makedirs(outdir, exist_ok=True)
+        styles_array = load_styles(s_input, n_seeds, device)
+        finder = DirectionFinder(
+            G, styles_array, build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip_loss_type),
+            IDLoss("a", device=device), resolution=resolution, batch_size=batch_size, learning_rate=learning_rate,
+            n_epochs=n_epochs, identity_loss_coef=identity_loss_coef, l2_reg_coef=l2_reg_coef,
+            clip_loss_coef=clip_loss_coef, noise_mode=noise_mode, seed=seed, world=world,
+            global_batch=batch_size * world.world_size if per_gpu_batch else batch_size,
+            init_delta=initial_delta(seed, init_std) if init_std > 0 else None)
+        if resume:
+            finder.load_direction(np.load(resume)["s"])
+        if world.rank == 0:
+            print(f"training param shape {tuple(finder.delta.shape)}")
+            print(f"Total number of iterations: {finder.total_iterations}")
+        t1 = time.time()
+        total = finder.total_iterations if max_iterations is None else min(max_iterations, finder.total_iterations)
+        for _ in range(total):
+            finder.step()
+            if world.rank == 0 and finder.it % 1000 == 999:
+                finder.save(f"{outdir}/direction_last.npz")
+            if world.rank == 0 and finder.it % 10 == 0:
+                print(finder.log_line())
+        if world.rank == 0:
+            finder.save(f'{outdir}/direction_{text_prompt.replace(" ", "_")}.npz')
+            print("time passed:", time.time() - t1)
+
+    return find_direction
+
+
+def main():
+    _cli()()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,41 @@
+"""Identity loss (id_loss/id_loss.py:7-39): 1 - <ArcFace(y_hat), ArcFace(y).detach()>, batch mean.
+
+``extract_feats``: adaptive-avg-pool to 256 (4x4 mean at 1024 px), crop [35:223, 32:220], adaptive pool
+to 112, IR-SE50, l2-normalised.  The target image's features are computed under no_grad (the reference detaches them, :32), so the
+backbone backward runs for y_hat only; the per-sample dot loop (id_loss.py:34-37) is a batched row dot.
+"""
+import os
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .model_irse import build_irse50
+
+
+class IDLoss(nn.Module):
+    def __init__(self, opts=None, facenet=None, weights="id_loss/model_ir_se50.pth", device="cuda", seed=3):
+        super().__init__()
+        if facenet is None:
+            sd = None
+            if weights and os.path.exists(weights):
+                sd = torch.load(weights, map_location="cpu", weights_only=True)
+            facenet = build_irse50(sd, seed=seed, device=device)
+        self.facenet = facenet.eval()
+        self.opts = opts
+
+    def extract_feats(self, x):
+        if x.shape[2] != 256:
+            x = F.adaptive_avg_pool2d(x, (256, 256))
+        x = x[:, :, 35:223, 32:220]
+        x = F.adaptive_avg_pool2d(x, (112, 112))
+        return self.facenet(x)
+
+    def per_sample(self, y_hat, y):
+        """(1 - <f(y_hat_i), f(y_i)>) for each i; y's features are detached."""
+        with torch.no_grad():
+            y_feats = self.extract_feats(y)
+        return 1 - (self.extract_feats(y_hat) * y_feats).sum(dim=1)
+
+    def forward(self, y_hat, y):
+        return self.per_sample(y_hat, y).mean(), 0.0

@@ -61,6 +61,44 @@ def generate_image(G, until_k, styles, temp_shapes, noise_mode="const", device=N
     return xs, img
 
 
+def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", delta=None,
+                        trainable=S_TRAINABLE_SPACE_CHANNELS):
+    """generate_image(G, until_k, styles + direction) where the direction lives only on `trainable` rows.
+
+    Same arithmetic as block_forward/generate_image, but each S row is passed to its layer as its own
+    tensor: only the rows that carry `delta` ([N or 1, len(trainable), 512]) require grad, so the
+    backward skips every style gradient find_direction does not use and stops below the first
+    trainable layer.  styles2[:, r] = styles[:, r] + delta[:, j] for r = trainable[j] (find_direction.py:307-308).
+    """
+    x = img = None
+    row = 0
+    for k, res in enumerate(G.synthesis.block_resolutions):
+        if k > until_k:
+            continue
+        block = getattr(G.synthesis, f"b{res}")
+        width = 2 if res == 4 else 3
+        rows = []
+        for j in range(width):
+            r = row + j
+            w = styles[:, r]
+            if delta is not None and r in trainable:
+                w = w + delta[:, trainable.index(r)]
+            rows.append(w)
+        shapes = temp_shapes[k]
+        if block.in_channels == 0:
+            x = block.const.to(torch.float32).unsqueeze(0).repeat([styles.shape[0], 1, 1, 1])
+            x = block.conv1(x, rows[0][..., :shapes[0]], noise_mode=noise_mode)
+        else:
+            x = block.conv0(x, rows[0][..., :shapes[0]], noise_mode=noise_mode)
+            x = block.conv1(x, rows[1][..., :shapes[1]], noise_mode=noise_mode)
+        if img is not None:
+            img = upfirdn2d.upsample2d(img, block.resample_filter)
+        y = block.torgb(x, rows[-1][..., :shapes[2]])
+        img = img.add_(y) if img is not None else y
+        row += width
+    return img
+
+
 def get_temp_shapes(G):
     shapes = []
     for res in G.synthesis.block_resolutions:
