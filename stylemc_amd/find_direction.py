@@ -63,8 +63,9 @@ class DirectionFinder:
 
     def __init__(self, G, styles_array, clip_losses, id_loss, resolution=1024, batch_size=4, learning_rate=1.5,
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
-                 seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None):
+                 seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None):
         self.G = G
+        self.synth_fn = synth_fn or utils.generate_image_rows   # (G, until_k, styles, shapes, noise, delta=)
         self.device = styles_array.device
         self.styles_array = styles_array
         self.clip_losses = clip_losses            # [(CLIPLoss, weight)], 'double' -> [(B/32, 1), (B/16, .5)]
@@ -101,9 +102,9 @@ class DirectionFinder:
         """Sum-form loss of this rank's shard: every per-sample term / global batch size."""
         T = S_TRAINABLE_SPACE_CHANNELS
         d = self.delta.detach().clone().requires_grad_(True)
-        img = utils.generate_image_rows(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+        img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
         with torch.no_grad():
-            orig = utils.generate_image_rows(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
+            orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
         id_terms = self.id_loss.per_sample(img, orig)
         src, tgt = unprocess(orig, self.mean, self.std), unprocess(img, self.mean, self.std)
         clip_terms = sum(w * cl.per_sample(src, tgt) for cl, w in self.clip_losses)

@@ -1,0 +1,91 @@
+"""Oracle-backed pieces that let stylemc_amd.find_direction.DirectionFinder run on the CPU in tests
+(multi-process gloo coverage) and provide the CPU reference for the GPU parity tests."""
+import torch
+
+from oracle import losses as OL
+from oracle import networks as ON
+from oracle import ops as O
+from stylemc_amd import synthetic
+from stylemc_amd.utils import S_TRAINABLE_SPACE_CHANNELS
+
+
+def oracle_generator(res, cbase, clamp=256.0, seed=0):
+    cfg = synthetic.generator_config(resolution=res, channel_base=cbase, conv_clamp=clamp)
+    sd = synthetic.generator_state_dict(cfg, seed=seed)
+    G = torch.nn.Module()
+    G.synthesis = ON.SynthesisNetwork(512, res, 3, channel_base=cbase, conv_clamp=clamp)
+    r = G.synthesis.load_state_dict({k[10:]: v for k, v in sd.items() if k.startswith("synthesis.")}, strict=False)
+    assert not r.unexpected_keys
+    return G.eval().requires_grad_(False)
+
+
+def oracle_rows_synth(G, until_k, styles, temp_shapes, noise_mode="const", delta=None, trainable=S_TRAINABLE_SPACE_CHANNELS):
+    """CPU twin of stylemc_amd.utils.generate_image_rows on oracle layers."""
+    x = img = None
+    row = 0
+    for k, res in enumerate(G.synthesis.block_resolutions):
+        if k > until_k:
+            continue
+        block = getattr(G.synthesis, f"b{res}")
+        width = 2 if res == 4 else 3
+        rows = []
+        for j in range(width):
+            w = styles[:, row + j]
+            if delta is not None and row + j in trainable:
+                w = w + delta[:, trainable.index(row + j)]
+            rows.append(w)
+        sh = temp_shapes[k]
+        if block.in_channels == 0:
+            x = block.const.unsqueeze(0).repeat([styles.shape[0], 1, 1, 1])
+            x = block.conv1(x, rows[0][..., :sh[0]], noise_mode=noise_mode)
+        else:
+            x = block.conv0(x, rows[0][..., :sh[0]], noise_mode=noise_mode)
+            x = block.conv1(x, rows[1][..., :sh[1]], noise_mode=noise_mode)
+        if img is not None:
+            img = O.upsample2d(img, block.resample_filter)
+        y = block.torgb(x, rows[-1][..., :sh[2]])
+        img = img + y if img is not None else y
+        row += width
+    return img
+
+
+class OracleID(torch.nn.Module):
+    def __init__(self, facenet):
+        super().__init__()
+        self.inner = OL.IDLoss(facenet)
+
+    def per_sample(self, y_hat, y):
+        f = self.inner.extract_feats(y).detach()
+        return 1 - (self.inner.extract_feats(y_hat) * f).sum(1)
+
+
+class OracleCLIP(torch.nn.Module):
+    def __init__(self, visual, text):
+        super().__init__()
+        self.inner = OL.CLIPLoss(visual, text)
+
+    def per_sample(self, src, tgt):
+        f = self.inner.visual(tgt) - self.inner.visual(src)
+        f = f / f.norm(dim=1, keepdim=True)
+        return 1 - torch.nn.functional.cosine_similarity(f, self.inner.text_features)
+
+
+class TinyFace(torch.nn.Module):
+    """Small stand-in for IR-SE50 (distributed-logic tests only): [N,3,112,112] -> unit [N,32]."""
+
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(0)
+        self.w1 = torch.nn.Parameter(torch.randn(8, 3, 5, 5, generator=g) * 0.2, requires_grad=False)
+        self.w2 = torch.nn.Parameter(torch.randn(32, 8 * 14 * 14, generator=g) * 0.02, requires_grad=False)
+
+    def forward(self, x):
+        x = torch.nn.functional.conv2d(x, self.w1, stride=4, padding=2).tanh()
+        x = torch.nn.functional.adaptive_avg_pool2d(x, 14).flatten(1) @ self.w2.t()
+        return x / x.norm(dim=1, keepdim=True)
+
+
+def tiny_clip_visual():
+    vis = OL.CLIPVisual(input_resolution=224, patch_size=32, width=64, layers=2, heads=2, output_dim=32).eval()
+    vis.load_state_dict(synthetic.seeded_state_dict(vis, seed=4))
+    return vis.requires_grad_(False)

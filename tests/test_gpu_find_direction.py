@@ -1,0 +1,74 @@
+"""End-to-end parity: the HIP find_direction (stylemc_amd.find_direction.DirectionFinder on the GPU)
+against the CPU oracle's restatement of the reference loop (oracle.find_direction) on identical
+seeded weights / styles / batch picks.  North-star tolerance: direction cosine similarity >= 0.999;
+per-iteration loss terms within rtol 1e-3; max-norm relative error of the direction <= 1e-2 (1024, 2 steps)
+/ 2e-2 (tiny generator, 4 steps) -- see _check for why the error grows with the step count."""
+import pytest
+import torch
+
+from oracle import find_direction as OF
+from oracle import losses as OL
+from oracle import synthesis as OS
+from stylemc_amd import synthetic
+from tests.fd_helpers import oracle_generator
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _run_pair(res, cbase, n_items, bs, iters):
+    from stylemc_amd import build, networks
+    from stylemc_amd.clip_loss import CLIPLoss
+    from stylemc_amd.find_direction import DirectionFinder, initial_delta
+    from stylemc_amd.id_loss import IDLoss
+    build.build(verbose=False)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    text = synthetic.text_direction("a photo of a face of a feminine woman", "a photo of a face of a man")
+    styles = synthetic.synthetic_styles(n_items, seed=5)
+    init = initial_delta(0, 0.01)
+    # CPU oracle
+    Go = oracle_generator(res, cbase, seed=0)
+    vis = OL.CLIPVisual().eval()
+    vis.load_state_dict(synthetic.seeded_state_dict(vis, seed=4))
+    net = OL.IRSE50().eval()
+    net.load_state_dict(synthetic.seeded_state_dict(net, seed=3))
+    log = []
+    sdir_o, delta_o = OF.find_direction(Go, styles, OL.CLIPLoss(vis.requires_grad_(False), text),
+                                        OL.IDLoss(net.requires_grad_(False)), OS.get_temp_shapes(Go),
+                                        res.bit_length() - 3, batch_size=bs, n_epochs=1, seed=2,
+                                        max_iterations=iters, log=log, init_delta=init)
+    # GPU build
+    cfg = synthetic.generator_config(resolution=res, channel_base=cbase)
+    G = networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=DEV)
+    f = DirectionFinder(G, styles.to(DEV), [(CLIPLoss(DEV, text_features=text, seed=4), 1.0)],
+                        IDLoss(device=DEV, weights=None, seed=3), resolution=res, batch_size=bs, n_epochs=1, seed=2,
+                        init_delta=init)
+    parts = []
+    for _ in range(iters):
+        parts.append(f.step()["parts"].cpu())
+    return (sdir_o, delta_o, log), (f.styles_direction.cpu(), f.delta.cpu(), parts)
+
+
+def _check(o, g, max_err):
+    sdir_o, delta_o, log = o
+    sdir_g, delta_g, parts = g
+    assert torch.isfinite(delta_g).all()
+    for it, (p, l) in enumerate(zip(parts, log)):
+        ref = torch.tensor([l["clip_loss"], l["identity_loss"], 0.0, l["l2_loss"]])
+        assert torch.allclose(p, ref, rtol=1e-3, atol=1e-5), (it, p, ref)
+    cos = torch.nn.functional.cosine_similarity(delta_g.double().flatten(), delta_o.double().flatten(), dim=0)
+    assert cos >= 0.999, f"direction cosine {cos.item():.6f}"
+    # The directional CLIP term normalises E(tgt) - E(src), a small difference of O(1) embeddings, so
+    # fp32 rounding differences (~1e-6 relative) grow to ~1e-3 per step in the gradient direction.
+    err = (delta_g - delta_o).abs().max() / delta_o.abs().max()
+    assert err <= max_err, f"direction max-norm rel err {err.item():.2e}"
+    assert (sdir_g - sdir_o).abs().max() <= max_err * sdir_o.abs().max()
+
+
+def test_find_direction_tiny_generator_vs_oracle():
+    _check(*_run_pair(32, 512, n_items=5, bs=2, iters=4), max_err=2e-2)
+
+
+def test_find_direction_ffhq1024_vs_oracle():
+    _check(*_run_pair(1024, 32768, n_items=3, bs=2, iters=2), max_err=1e-2)
