@@ -128,6 +128,14 @@ int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_stride, f
                              int t_w, int y_h, int y_w, const float* f, int fh, int fw, int padx0, int pady0,
                              float fgain, int flip, const smc_conv_epilogue* epi, void* stream);
 
+/* Backward of smc_modconv_blur_act_f32 in one pass: du = bias_act'(g; y re-derived from u) * d[n,o],
+ * dt = adjoint FIR of du (pad (pady0, padx0) = (fh-1-p, fw-1-p) of the forward pad p, flip, gain fgain;
+ * upfirdn2d.py:245-264 rule), and if dd != NULL: dd[n,o] += sum_hw dz*u.  g/u: [n,c,u_h,u_w],
+ * dt: [n,c,t_h,t_w].  4x4 filters only (SMC_ERR_UNSUPPORTED otherwise). */
+int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* dt, float* dd, int n, int c, int u_h, int u_w,
+                                 int t_h, int t_w, const float* f, int fh, int fw, int padx0, int pady0, float fgain,
+                                 int flip, const smc_conv_epilogue* epi, void* stream);
+
 /* d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps), wsq[o,i] = sum_k W[o,i,k]^2 (demodulation). */
 int smc_modconv_demod_f32(const float* s, const float* wsq, float* d, int n, int cin, int cout, float eps,
                           void* stream);

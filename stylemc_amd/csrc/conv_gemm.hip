@@ -23,7 +23,7 @@
 
 namespace {
 
-constexpr int BK = 16;
+constexpr int BK = 16;   // K-step granularity the host requires (cin % 16 == 0)
 constexpr int NT = 256;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -57,18 +57,19 @@ struct GemmParams {
     int64_t split_stride;
 };
 
-template <int WO, int WM, int TO, int TM>
+template <int WO, int WM, int TO, int TM, int BKT>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
     static_assert(WO * WM == 4, "4 waves");
     constexpr int BO = WO * TO * 32;
     constexpr int BM = WM * TM * 32;
-    constexpr int XR = BK * BM / NT;         // input-tile rows loaded per thread
-    constexpr int WV = BK * BO / 4;          // float4 vectors in the weight tile
-    static_assert(NT % BM == 0 || BM % NT == 0, "thread->position map");
-    static_assert(BM <= NT, "one position per thread");
+    constexpr int XR = BKT * BM / NT;        // input-tile rows (channels) loaded per thread
+    constexpr int WV = BKT * BO / 4;         // float4 vectors in the weight tile
+    constexpr int WPT = (WV + NT - 1) / NT;  // float4 weight vectors per thread
+    constexpr int TILE = BKT * (BO + BM);    // floats per LDS stage
+    static_assert(NT % BM == 0 && XR % 4 == 0, "thread->position map");
 
-    __shared__ float Ws[BK][BO];
-    __shared__ float Xs[BK][BM];
+    // One LDS array, two stages: [stage][ Ws[BKT][BO] | Xs[BKT][BM] ]
+    __shared__ float smem[2 * TILE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
     if (m0 >= M) return;  // uniform: grid is sized for the largest phase
     const int o0 = blockIdx.y * BO;
 
-    const int cpk = p.cin / BK;  // channel chunks per tap
+    const int cpk = p.cin / BKT;  // channel chunks per tap
     const int ks_total = ph.ntaps * cpk;
     const int ks_begin = (int)((int64_t)ks_total * split / p.nsplit);
     const int ks_end = (int)((int64_t)ks_total * (split + 1) / p.nsplit);
@@ -102,25 +103,27 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
         b = rem - a * ph.out_w;
     }
     const int64_t in_hw = (int64_t)p.in_h * p.in_w;
-    const float* xbase = p.x + (int64_t)nn * p.cin * in_hw;
-    const float* sbase = p.s ? p.s + (int64_t)nn * p.cin : nullptr;
+    const float* xbase = p.x + (int64_t)nn * p.cin * in_hw + (int64_t)kr0 * in_hw;
+    const float* sbase = p.s ? p.s + (int64_t)nn * p.cin + kr0 : nullptr;
     const int ay = a * ph.in_stride, bx = b * ph.in_stride;
 
     float xr[XR];
-    constexpr int WPT = (WV + NT - 1) / NT;  // float4 weight vectors per thread
     float4 wr[WPT];
 
     auto load_step = [&](int ks) {
         const int t = ks / cpk;
-        const int ci0 = (ks - t * cpk) * BK;
+        const int ci0 = (ks - t * cpk) * BKT;
         const int iy = ay + ph.dy[t], ix = bx + ph.dx[t];
         const bool ok = mvalid && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w;
-        const float* src = xbase + (int64_t)(ci0 + kr0) * in_hw + (ok ? (int64_t)iy * p.in_w + ix : 0);
+        const float* src = xbase + (int64_t)ci0 * in_hw + (ok ? (int64_t)iy * p.in_w + ix : 0);
 #pragma unroll
-        for (int r = 0; r < XR; ++r) {
-            float v = ok ? src[r * in_hw] : 0.f;
-            if (sbase) v *= sbase[ci0 + kr0 + r];
-            xr[r] = v;
+        for (int r = 0; r < XR; ++r) xr[r] = ok ? src[r * in_hw] : 0.f;
+        if (sbase) {
+#pragma unroll
+            for (int r = 0; r < XR; r += 4) {
+                const float4 sv = *reinterpret_cast<const float4*>(sbase + ci0 + r);
+                xr[r] *= sv.x; xr[r + 1] *= sv.y; xr[r + 2] *= sv.z; xr[r + 3] *= sv.w;
+            }
         }
 #pragma unroll
         for (int q = 0; q < WPT; ++q) {
@@ -133,6 +136,18 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
             wr[q] = val;
         }
     };
+    auto store_step = [&](int stage) {
+        float* Ws = smem + stage * TILE;
+        float* Xs = Ws + BKT * BO;
+#pragma unroll
+        for (int r = 0; r < XR; ++r) Xs[(kr0 + r) * BM + ml] = xr[r];
+#pragma unroll
+        for (int q = 0; q < WPT; ++q) {
+            const int v = tid + q * NT;
+            const int wkk = v / (BO / 4), wc4 = v - wkk * (BO / 4);
+            if (v < WV) *reinterpret_cast<float4*>(&Ws[wkk * BO + wc4 * 4]) = wr[q];
+        }
+    };
 
     f32x16 acc[TO][TM];
 #pragma unroll
@@ -142,33 +157,34 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    if (ks_begin < ks_end) load_step(ks_begin);
     const int kh = lane >> 5, l32 = lane & 31;
+    int stage = 0;
+    if (ks_begin < ks_end) {
+        load_step(ks_begin);
+        store_step(0);
+    }
+    __syncthreads();
     for (int ks = ks_begin; ks < ks_end; ++ks) {
+        const bool more = ks + 1 < ks_end;
+        if (more) load_step(ks + 1);  // global loads stay in flight under the MFMAs below
+        const float* Ws = smem + stage * TILE;
+        const float* Xs = Ws + BKT * BO;
 #pragma unroll
-        for (int r = 0; r < XR; ++r) Xs[kr0 + r][ml] = xr[r];
-#pragma unroll
-        for (int q = 0; q < WPT; ++q) {
-            const int v = tid + q * NT;
-            const int wkk = v / (BO / 4), wc4 = v - wkk * (BO / 4);
-            if (v < WV) *reinterpret_cast<float4*>(&Ws[wkk][wc4 * 4]) = wr[q];
-        }
-        __syncthreads();
-        if (ks + 1 < ks_end) load_step(ks + 1);
-#pragma unroll
-        for (int kk = 0; kk < BK; kk += 2) {
+        for (int kk = 0; kk < BKT; kk += 2) {
             float af[TO], bf[TM];
 #pragma unroll
-            for (int i = 0; i < TO; ++i) af[i] = Ws[kk + kh][wo * TO * 32 + i * 32 + l32];
+            for (int i = 0; i < TO; ++i) af[i] = Ws[(kk + kh) * BO + wo * TO * 32 + i * 32 + l32];
 #pragma unroll
-            for (int j = 0; j < TM; ++j) bf[j] = Xs[kk + kh][wm * TM * 32 + j * 32 + l32];
+            for (int j = 0; j < TM; ++j) bf[j] = Xs[(kk + kh) * BM + wm * TM * 32 + j * 32 + l32];
 #pragma unroll
             for (int i = 0; i < TO; ++i)
 #pragma unroll
                 for (int j = 0; j < TM; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
         }
+        if (more) store_step(stage ^ 1);  // the other stage was last read before the previous barrier
         __syncthreads();
+        stage ^= 1;
     }
 
     // ---- epilogue: lane owns column m, registers walk output channels
@@ -326,9 +342,20 @@ SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w
 
     hipStream_t st = smc::as_stream(stream);
     dim3 grid((unsigned)smc::ceil_div(max_m, c.bm), (unsigned)smc::ceil_div(cout, c.bo), (unsigned)(nphases * nsplit));
-    if (cfg == 0) hipLaunchKernelGGL((conv_gemm_kernel<2, 2, 2, 2>), grid, dim3(NT), 0, st, p);
-    else if (cfg == 1) hipLaunchKernelGGL((conv_gemm_kernel<1, 4, 2, 2>), grid, dim3(NT), 0, st, p);
-    else hipLaunchKernelGGL((conv_gemm_kernel<1, 4, 1, 2>), grid, dim3(NT), 0, st, p);
+    // BK=32 halves the barriers per FLOP; it pays on the long-K 512-channel layers, BK=16 (more
+    // workgroups per CU: 32-40 KB LDS vs 64-80 KB) on the high-resolution ones (tools/bench_gemm.py).
+    bool k32 = cin % 32 == 0 && cin >= 512;
+    if (const char* f = getenv("SMC_FORCE_BK")) k32 = k32 && atoi(f) != 16;  // A/B knob (tools/bench_gemm.py)
+    if (cfg == 0) {
+        if (k32) hipLaunchKernelGGL((conv_gemm_kernel<2, 2, 2, 2, 32>), grid, dim3(NT), 0, st, p);
+        else hipLaunchKernelGGL((conv_gemm_kernel<2, 2, 2, 2, 16>), grid, dim3(NT), 0, st, p);
+    } else if (cfg == 1) {
+        if (k32) hipLaunchKernelGGL((conv_gemm_kernel<1, 4, 2, 2, 32>), grid, dim3(NT), 0, st, p);
+        else hipLaunchKernelGGL((conv_gemm_kernel<1, 4, 2, 2, 16>), grid, dim3(NT), 0, st, p);
+    } else {
+        if (k32) hipLaunchKernelGGL((conv_gemm_kernel<1, 4, 1, 2, 32>), grid, dim3(NT), 0, st, p);
+        else hipLaunchKernelGGL((conv_gemm_kernel<1, 4, 1, 2, 16>), grid, dim3(NT), 0, st, p);
+    }
     rc = smc::check_launch("smc_conv_gemm_f32");
     if (rc != SMC_OK || nsplit == 1) return rc;
     return smc_modconv_epilogue_f32(workspace, nsplit, plane_elems, y, n, cout, y_h, y_w, &e, stream);

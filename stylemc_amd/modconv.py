@@ -190,21 +190,22 @@ class ModConvFn(torch.autograd.Function):
         if not (need_dx or need_ds):
             return None, None, None, None, None, None, None
         gy = gy.contiguous()
-        du = torch.empty_like(u)
         dd = torch.zeros(n, P.cout, device=x.device, dtype=torch.float32) if (need_ds and spec.demodulate) else None
         epi = _epilogue(_hip.EPI_MODACT, d, ctx.noise, ctx.nstride, ctx.strength, spec.bias, spec.act, spec.alpha,
                         ctx.gain, ctx.clamp)
-        _hip.call("smc_modconv_act_bwd_f32", gy.data_ptr(), u.data_ptr(), du.data_ptr(), _hip.ptr(dd), n, P.cout,
-                  u.shape[2], u.shape[3], ctypes.byref(epi), _hip.stream())
-        g = du
-        if spec.up == 2:
+        if spec.up == 1:
+            g = torch.empty_like(u)
+            _hip.call("smc_modconv_act_bwd_f32", gy.data_ptr(), u.data_ptr(), g.data_ptr(), _hip.ptr(dd), n, P.cout,
+                      u.shape[2], u.shape[3], ctypes.byref(epi), _hip.stream())
+        else:
+            # fused: epilogue backward + adjoint of FIR(pad 1, gain 4) (pad fw-1-1 = 2, correlation) + dd
             f = spec.filter.to(x.device)
             fh, fw = f.shape
             th, tw = 2 * h + 1, 2 * w + 1
             g = torch.empty(n, P.cout, th, tw, device=x.device, dtype=torch.float32)
-            # adjoint of FIR(pad 1, gain 4): pad (fw - 1 - 1) = 2 on both sides, correlation (upfirdn2d.py:251-261)
-            _hip.call("smc_upfirdn2d_f32", du.data_ptr(), _hip.ptr(f), g.data_ptr(), n * P.cout, du.shape[2],
-                      du.shape[3], th, tw, fh, fw, 1, 1, 1, 1, fw - 2, fw - 2, fh - 2, fh - 2, 1, 4.0, _hip.stream())
+            _hip.call("smc_modconv_blur_act_bwd_f32", gy.data_ptr(), u.data_ptr(), g.data_ptr(), _hip.ptr(dd), n,
+                      P.cout, u.shape[2], u.shape[3], th, tw, _hip.ptr(f), fh, fw, fw - 2, fh - 2, 4.0, 1,
+                      ctypes.byref(epi), _hip.stream())
         dx = torch.empty_like(x) if need_dx else None
         dxs = torch.empty_like(x) if need_ds else None
         if need_dx:
