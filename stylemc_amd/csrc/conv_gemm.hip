@@ -107,45 +107,52 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
     const float* sbase = p.s ? p.s + (int64_t)nn * p.cin + kr0 : nullptr;
     const int ay = a * ph.in_stride, bx = b * ph.in_stride;
 
+    // Prefetch registers.  Loads are unconditional (out-of-image taps read a valid dummy address) and
+    // the style scale / zero mask is applied only when the tile is written to LDS, after the MFMAs:
+    // nothing consumes a loaded value before the next barrier, so the loads overlap the whole step.
     float xr[XR];
+    float4 sr[XR / 4];
     float4 wr[WPT];
+    bool xok = false;
+    const bool has_s = p.s != nullptr;
+    const float* swhere = has_s ? sbase : p.x;  // any valid address when there is no scale
 
     auto load_step = [&](int ks) {
         const int t = ks / cpk;
         const int ci0 = (ks - t * cpk) * BKT;
         const int iy = ay + ph.dy[t], ix = bx + ph.dx[t];
-        const bool ok = mvalid && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w;
-        const float* src = xbase + (int64_t)ci0 * in_hw + (ok ? (int64_t)iy * p.in_w + ix : 0);
+        xok = mvalid && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w;
+        const float* src = xbase + (int64_t)ci0 * in_hw + (xok ? (int64_t)iy * p.in_w + ix : 0);
 #pragma unroll
-        for (int r = 0; r < XR; ++r) xr[r] = ok ? src[r * in_hw] : 0.f;
-        if (sbase) {
+        for (int r = 0; r < XR; ++r) xr[r] = src[r * in_hw];
 #pragma unroll
-            for (int r = 0; r < XR; r += 4) {
-                const float4 sv = *reinterpret_cast<const float4*>(sbase + ci0 + r);
-                xr[r] *= sv.x; xr[r + 1] *= sv.y; xr[r + 2] *= sv.z; xr[r + 3] *= sv.w;
-            }
-        }
+        for (int r = 0; r < XR; r += 4) sr[r / 4] = *reinterpret_cast<const float4*>(swhere + (has_s ? ci0 + r : 0));
 #pragma unroll
         for (int q = 0; q < WPT; ++q) {
-            const int v = tid + q * NT;
+            int v = tid + q * NT;
+            v = v < WV ? v : v - WV;  // surplus threads re-read a valid vector; the store skips them
             const int wkk = v / (BO / 4), wc4 = v - wkk * (BO / 4);
             const int o = o0 + wc4 * 4;
-            float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (v < WV && o < p.cout)  // cout is a multiple of 16: a float4 never straddles the edge
-                val = *reinterpret_cast<const float4*>(ph.wk + ((int64_t)t * p.cin + ci0 + wkk) * p.cout + o);
-            wr[q] = val;
+            wr[q] = *reinterpret_cast<const float4*>(ph.wk + ((int64_t)t * p.cin + ci0 + wkk) * p.cout +
+                                                     (o < p.cout ? o : 0));
         }
     };
     auto store_step = [&](int stage) {
         float* Ws = smem + stage * TILE;
         float* Xs = Ws + BKT * BO;
 #pragma unroll
-        for (int r = 0; r < XR; ++r) Xs[(kr0 + r) * BM + ml] = xr[r];
+        for (int r = 0; r < XR; ++r) {
+            const float4 sv = sr[r / 4];
+            const float sc = has_s ? ((r & 3) == 0 ? sv.x : (r & 3) == 1 ? sv.y : (r & 3) == 2 ? sv.z : sv.w) : 1.f;
+            Xs[(kr0 + r) * BM + ml] = xok ? xr[r] * sc : 0.f;
+        }
 #pragma unroll
         for (int q = 0; q < WPT; ++q) {
             const int v = tid + q * NT;
             const int wkk = v / (BO / 4), wc4 = v - wkk * (BO / 4);
-            if (v < WV) *reinterpret_cast<float4*>(&Ws[wkk * BO + wc4 * 4]) = wr[q];
+            float4 w = wr[q];
+            if (o0 + wc4 * 4 >= p.cout) w = make_float4(0.f, 0.f, 0.f, 0.f);  // cout = 16 in a 32-wide tile
+            if (v < WV) *reinterpret_cast<float4*>(&Ws[wkk * BO + wc4 * 4]) = w;
         }
     };
 
@@ -169,18 +176,28 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
         if (more) load_step(ks + 1);  // global loads stay in flight under the MFMAs below
         const float* Ws = smem + stage * TILE;
         const float* Xs = Ws + BKT * BO;
+        // All fragments of a 16-deep chunk are read first, pinned ahead of the MFMAs by a scheduling
+        // barrier: the LDS latency is then paid once per chunk (counted lgkmcnt waits), not per k-pair.
+        const float* wrow = Ws + kh * BO + wo * TO * 32 + l32;
+        const float* xrow = Xs + kh * BM + wm * TM * 32 + l32;
 #pragma unroll
-        for (int kk = 0; kk < BKT; kk += 2) {
-            float af[TO], bf[TM];
+        for (int k0 = 0; k0 < BKT; k0 += 16) {
+            float af[8][TO], bf[8][TM];
 #pragma unroll
-            for (int i = 0; i < TO; ++i) af[i] = Ws[(kk + kh) * BO + wo * TO * 32 + i * 32 + l32];
+            for (int q = 0; q < 8; ++q) {
 #pragma unroll
-            for (int j = 0; j < TM; ++j) bf[j] = Xs[(kk + kh) * BM + wm * TM * 32 + j * 32 + l32];
+                for (int i = 0; i < TO; ++i) af[q][i] = wrow[(k0 + 2 * q) * BO + i * 32];
 #pragma unroll
-            for (int i = 0; i < TO; ++i)
+                for (int j = 0; j < TM; ++j) bf[q][j] = xrow[(k0 + 2 * q) * BM + j * 32];
+            }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int j = 0; j < TM; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+            for (int q = 0; q < 8; ++q)
+#pragma unroll
+                for (int i = 0; i < TO; ++i)
+#pragma unroll
+                    for (int j = 0; j < TM; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q][i], bf[q][j], acc[i][j], 0, 0, 0);
         }
         if (more) store_step(stage ^ 1);  // the other stage was last read before the previous barrier
         __syncthreads();

@@ -352,25 +352,31 @@ __global__ __launch_bounds__(256) void channel_dot_kernel(const float* a, const 
 
 // ---------------------------------------------------------------------------------------------- demod bwd
 
+// 32 input channels x 8 output-channel groups per workgroup; each thread sums a strided slice of o
+// (coalesced 128-B rows of Wsq), then the 8 partials are reduced through LDS.
 __global__ __launch_bounds__(256) void demod_bwd_kernel(const float* s, const float* d, const float* dd,
                                                         const float* wsq, float* ds, int cin, int cout) {
-    __shared__ float coef[256];
+    __shared__ float part[8][33];
     const int nn = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int il = threadIdx.x & 31, og = threadIdx.x >> 5;
+    const int i = blockIdx.x * 32 + il;
+    const float* dp = d + (int64_t)nn * cout;
+    const float* ddp = dd + (int64_t)nn * cout;
     float acc = 0.f;
-    for (int o0 = 0; o0 < cout; o0 += 256) {
-        __syncthreads();
-        const int o = o0 + threadIdx.x;
-        if (o < cout) {
-            const float dv = d[(int64_t)nn * cout + o];
-            coef[threadIdx.x] = dd[(int64_t)nn * cout + o] * dv * dv * dv;
+    if (i < cin) {
+        for (int o = og; o < cout; o += 8) {
+            const float dv = dp[o];
+            acc += ddp[o] * dv * dv * dv * wsq[(int64_t)o * cin + i];
         }
-        __syncthreads();
-        const int lim = cout - o0 < 256 ? cout - o0 : 256;
-        if (i < cin)
-            for (int k = 0; k < lim; ++k) acc += coef[k] * wsq[(int64_t)(o0 + k) * cin + i];
     }
-    if (i < cin) ds[(int64_t)nn * cin + i] += -s[(int64_t)nn * cin + i] * acc;
+    part[og][il] = acc;
+    __syncthreads();
+    if (og == 0 && i < cin) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t += part[k][il];
+        ds[(int64_t)nn * cin + i] += -s[(int64_t)nn * cin + i] * t;
+    }
 }
 
 int64_t grid_cap(int64_t blocks) {
@@ -450,7 +456,7 @@ SMC_API int smc_modconv_demod_bwd_f32(const float* s, const float* d, const floa
                                       int n, int cin, int cout, void* stream) {
     SMC_CHECK(s && d && dd && wsq && ds && n >= 1 && cin >= 1 && cout >= 1, "smc_modconv_demod_bwd_f32: bad args");
     SMC_CHECK(n < 65536, "smc_modconv_demod_bwd_f32: batch too large");
-    hipLaunchKernelGGL(demod_bwd_kernel, dim3((unsigned)smc::ceil_div(cin, 256), (unsigned)n), dim3(256), 0,
+    hipLaunchKernelGGL(demod_bwd_kernel, dim3((unsigned)smc::ceil_div(cin, 32), (unsigned)n), dim3(256), 0,
                        smc::as_stream(stream), s, d, dd, wsq, ds, cin, cout);
     return smc::check_launch("smc_modconv_demod_bwd_f32");
 }

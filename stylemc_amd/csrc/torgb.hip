@@ -31,7 +31,31 @@ __global__ __launch_bounds__(256) void torgb_fwd_kernel(const float* x, const fl
     for (int c = 0; c < kMaxOut; ++c)
 #pragma unroll
         for (int v = 0; v < V; ++v) acc[c][v] = 0.f;
-    for (int k = 0; k < cin; ++k) {
+    // 8 channels per round: the 8 independent 16-B loads are all in flight before the first FMA.
+    constexpr int U = 8;
+    int k = 0;
+    for (; k + U <= cin; k += U) {
+        float xv[U][V];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (VEC) {
+                const float4 t = *reinterpret_cast<const float4*>(xp + (int64_t)(k + u) * hw + p0);
+                xv[u][0] = t.x; xv[u][V > 1 ? 1 : 0] = t.y; xv[u][V > 2 ? 2 : 0] = t.z; xv[u][V > 3 ? 3 : 0] = t.w;
+            } else {
+                xv[u][0] = xp[(int64_t)(k + u) * hw + p0];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < kMaxOut; ++c) {
+                if (c >= cout) break;
+                const float wv = ws[c * cin + k + u];
+#pragma unroll
+                for (int v = 0; v < V; ++v) acc[c][v] += wv * xv[u][v];
+            }
+    }
+    for (; k < cin; ++k) {
         float xv[V];
         if (VEC) {
             const float4 t = *reinterpret_cast<const float4*>(xp + (int64_t)k * hw + p0);

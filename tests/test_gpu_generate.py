@@ -1,0 +1,77 @@
+"""generate_fromS (pairs with the reference's in-place drift, and the video sweep) and seeds -> W -> S on
+the GPU vs the CPU oracle.  Per-pixel tolerance on the uint8 images (generate_fromS.py:174-175 truncates):
+|diff| <= 1 everywhere and >= 99.9 % of pixels exact (fp32 summation order can move a value across an
+integer boundary)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import generate_fromS as OG
+from oracle import networks as ON
+from oracle import synthesis as OS
+from stylemc_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _pair(res, cbase):
+    from stylemc_amd import build, networks
+    build.build(verbose=False)
+    cfg = synthetic.generator_config(resolution=res, channel_base=cbase)
+    sd = synthetic.generator_state_dict(cfg, seed=0)
+    G = networks.build_generator(cfg, sd, device=DEV)
+    Go = ON.Generator(512, 0, 512, res, 3, channel_base=cbase, conv_clamp=cfg["conv_clamp"])
+    r = Go.load_state_dict(sd, strict=False)
+    assert not r.unexpected_keys
+    return G, Go.eval().requires_grad_(False)
+
+
+def _check_u8(a, b, what):
+    a = a.cpu().numpy().astype(np.int16)
+    b = b.numpy().astype(np.int16)
+    diff = np.abs(a - b)
+    assert diff.max() <= 1, f"{what}: max |diff| {diff.max()}"
+    assert (diff == 0).mean() >= 0.999, f"{what}: exact fraction {(diff == 0).mean():.5f}"
+
+
+@pytest.mark.parametrize("res,cbase,n", [(32, 512, 4), (1024, 32768, 2)])
+def test_generate_fromS_pairs_vs_oracle(res, cbase, n):
+    from stylemc_amd import generate_fromS, utils
+    G, Go = _pair(res, cbase)
+    styles = synthetic.synthetic_styles(n, seed=9)
+    direction = torch.zeros(1, 26, 512)
+    direction[:, utils.S_TRAINABLE_SPACE_CHANNELS] = torch.randn(1, 8, 512, generator=torch.Generator().manual_seed(1)) * 0.3
+    got = list(generate_fromS.render_pairs(G, styles.to(DEV), direction.to(DEV), 2.0, utils.get_temp_shapes(G)))
+    ref = OG.render_pairs(Go, styles.clone(), direction, 2.0, OS.get_temp_shapes(Go))
+    for (i, imgs), rimgs in zip(got, ref):
+        for k in range(2):
+            _check_u8(imgs[k], rimgs[k], f"item {i} power {k}")
+
+
+def test_generate_fromS_video_sweep_vs_oracle():
+    from stylemc_amd import generate_fromS, utils
+    G, Go = _pair(1024, 32768)
+    style_row = synthetic.synthetic_styles(1, seed=3)[0]
+    direction = torch.zeros(1, 26, 512)
+    direction[:, utils.S_TRAINABLE_SPACE_CHANNELS] = torch.randn(1, 8, 512, generator=torch.Generator().manual_seed(2)) * 0.1
+    powers = np.linspace(0.0, 50.0, 5)
+    got = generate_fromS.render_sweep(G, style_row.to(DEV), direction.to(DEV), powers, utils.get_temp_shapes(G),
+                                      batch=4)
+    ref = OG.render_sweep(Go, style_row, direction, powers, OS.get_temp_shapes(Go))
+    assert got.shape == (5, 1024, 1024, 3)
+    _check_u8(got, ref, "sweep")
+
+
+def test_seeds_to_w_to_s_vs_oracle():
+    from stylemc_amd import w_s
+    G, Go = _pair(1024, 32768)
+    seeds = [1, 2, 129]
+    ws = w_s.seeds_to_w(G, seeds, truncation_psi=0.7)
+    with torch.no_grad():
+        ws_o = Go.mapping(synthetic.seed_latents(seeds), None, truncation_psi=0.7)
+    np.testing.assert_allclose(ws.cpu().numpy(), ws_o.numpy(), rtol=1e-4, atol=1e-4 * ws_o.abs().max().item())
+    s = w_s.w_to_s(G, ws)
+    s_o, _ = OS.get_styles(Go, ws_o)
+    assert s.shape == (3, 26, 512)
+    np.testing.assert_allclose(s.cpu().numpy(), s_o.numpy(), rtol=1e-4, atol=1e-4 * s_o.abs().max().item())

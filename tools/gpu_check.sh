@@ -8,7 +8,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 python -m stylemc_amd.build > $OUT/build.log 2>&1 || { echo "BUILD FAILED"; tail -20 $OUT/build.log; exit 1; }
 if [ "$MODE" = "tests" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q --timeout=600 -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -m pytest tests -m gpu -q --timeout=600 --durations=8 -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
   rc=$?
   tail -3 $OUT/pytest_gpu.log
   grep -E "^E   " $OUT/pytest_gpu.log | head -10
