@@ -28,12 +28,18 @@ class CLIPLoss(nn.Module):
     def encode_image(self, image):
         return self.visual(image)
 
-    def per_sample(self, src_image, tgt_image):
-        with torch.no_grad():
-            src = self.visual(src_image)
-        f = self.visual(tgt_image) - src
+    @torch.no_grad()
+    def encode_src(self, src_image):
+        """E(src): the original image's embedding (no gradient flows to it in the reference)."""
+        return self.visual(src_image)
+
+    def per_sample_with(self, src_emb, tgt_image):
+        f = self.visual(tgt_image) - src_emb
         f = f / f.norm(dim=1, keepdim=True)
         return 1 - F.cosine_similarity(f, self.text_features)
+
+    def per_sample(self, src_image, tgt_image):
+        return self.per_sample_with(self.encode_src(src_image), tgt_image)
 
     def forward(self, src_image, tgt_image):
         return self.per_sample(src_image, tgt_image).mean()

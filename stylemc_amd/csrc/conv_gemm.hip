@@ -57,7 +57,7 @@ struct GemmParams {
     int64_t split_stride;
 };
 
-template <int WO, int WM, int TO, int TM, int BKT>
+template <int WO, int WM, int TO, int TM, int BKT, bool BUF>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
     static_assert(WO * WM == 4, "4 waves");
     constexpr int BO = WO * TO * 32;
@@ -107,26 +107,49 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
     const float* sbase = p.s ? p.s + (int64_t)nn * p.cin + kr0 : nullptr;
     const int ay = a * ph.in_stride, bx = b * ph.in_stride;
 
-    // Prefetch registers.  Loads are unconditional (out-of-image taps read a valid dummy address) and
-    // the style scale / zero mask is applied only when the tile is written to LDS, after the MFMAs:
-    // nothing consumes a loaded value before the next barrier, so the loads overlap the whole step.
+    // Prefetch registers.  Loads are unconditional and nothing consumes a loaded value before the
+    // next barrier, so the loads overlap the whole step's MFMAs; the style scale is applied when the
+    // tile is written to LDS.
+    //  * input tile: raw buffer loads -- per-thread 32-bit voffset (position) + wave-uniform soffset
+    //    (channel row), so each load costs no VALU address math; an out-of-image tap gets a voffset
+    //    beyond the buffer and the hardware range check returns 0 (no select, no branch).
+    //  * style scale: when a workgroup's positions lie in one image (hw_out % BM == 0) s[n, i] scales
+    //    the BKT x BO weight tile (BO/BM of the multiplies of scaling the input tile).
     float xr[XR];
     float4 sr[XR / 4];
     float4 wr[WPT];
+    float ws_[WPT];
     bool xok = false;
     const bool has_s = p.s != nullptr;
-    const float* swhere = has_s ? sbase : p.x;  // any valid address when there is no scale
+    const bool s_on_w = has_s && hw_out % BM == 0;
+    const bool s_on_x = has_s && !s_on_w;
+    const float* swhere = s_on_x ? sbase : p.x;  // any valid address when unused
+    const float* sblk = s_on_w ? p.s + (int64_t)(m0 / hw_out) * p.cin : p.x;
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, (short)0, (int)(BUF ? (int64_t)p.n * p.cin * in_hw * 4 : 0), 0x00020000);
+    const int xvbase = (int)(((int64_t)nn * p.cin + kr0) * in_hw) * 4;
 
     auto load_step = [&](int ks) {
         const int t = ks / cpk;
         const int ci0 = (ks - t * cpk) * BKT;
         const int iy = ay + ph.dy[t], ix = bx + ph.dx[t];
         xok = mvalid && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w;
-        const float* src = xbase + (int64_t)ci0 * in_hw + (xok ? (int64_t)iy * p.in_w + ix : 0);
+        if constexpr (BUF) {
+            const int voff = xok ? xvbase + (iy * p.in_w + ix) * 4 : 0x7ffffff0;
+            const int srow = ci0 * (int)in_hw * 4;
 #pragma unroll
-        for (int r = 0; r < XR; ++r) xr[r] = src[r * in_hw];
+            for (int r = 0; r < XR; ++r)
+                xr[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                      xrsrc, voff, srow + r * (int)in_hw * 4, 0));
+        } else {
+            const float* src = xbase + (int64_t)ci0 * in_hw + (xok ? (int64_t)iy * p.in_w + ix : 0);
 #pragma unroll
-        for (int r = 0; r < XR; r += 4) sr[r / 4] = *reinterpret_cast<const float4*>(swhere + (has_s ? ci0 + r : 0));
+            for (int r = 0; r < XR; ++r) xr[r] = src[r * in_hw];
+        }
+        if (s_on_x) {
+#pragma unroll
+            for (int r = 0; r < XR; r += 4) sr[r / 4] = *reinterpret_cast<const float4*>(swhere + ci0 + r);
+        }
 #pragma unroll
         for (int q = 0; q < WPT; ++q) {
             int v = tid + q * NT;
@@ -135,6 +158,7 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
             const int o = o0 + wc4 * 4;
             wr[q] = *reinterpret_cast<const float4*>(ph.wk + ((int64_t)t * p.cin + ci0 + wkk) * p.cout +
                                                      (o < p.cout ? o : 0));
+            ws_[q] = s_on_w ? sblk[ci0 + wkk] : 1.f;
         }
     };
     auto store_step = [&](int stage) {
@@ -142,16 +166,21 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
         float* Xs = Ws + BKT * BO;
 #pragma unroll
         for (int r = 0; r < XR; ++r) {
-            const float4 sv = sr[r / 4];
-            const float sc = has_s ? ((r & 3) == 0 ? sv.x : (r & 3) == 1 ? sv.y : (r & 3) == 2 ? sv.z : sv.w) : 1.f;
-            Xs[(kr0 + r) * BM + ml] = xok ? xr[r] * sc : 0.f;
+            float v = xr[r];
+            if (s_on_x) {
+                const float4 sv = sr[r / 4];
+                v *= (r & 3) == 0 ? sv.x : (r & 3) == 1 ? sv.y : (r & 3) == 2 ? sv.z : sv.w;
+            }
+            if constexpr (!BUF) v = xok ? v : 0.f;
+            Xs[(kr0 + r) * BM + ml] = v;
         }
 #pragma unroll
         for (int q = 0; q < WPT; ++q) {
             const int v = tid + q * NT;
             const int wkk = v / (BO / 4), wc4 = v - wkk * (BO / 4);
             float4 w = wr[q];
-            if (o0 + wc4 * 4 >= p.cout) w = make_float4(0.f, 0.f, 0.f, 0.f);  // cout = 16 in a 32-wide tile
+            const float sc = (o0 + wc4 * 4 >= p.cout) ? 0.f : ws_[q];  // 0: cout = 16 in a 32-wide tile
+            w.x *= sc; w.y *= sc; w.z *= sc; w.w *= sc;
             if (v < WV) *reinterpret_cast<float4*>(&Ws[wkk * BO + wc4 * 4]) = w;
         }
     };
@@ -241,6 +270,277 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Phase-fused stride-2 transposed 3x3 conv (the up=2 layers' conv, conv2d_resample.py:125-138).
+// T[o, 2a+py, 2b+px] = sum over the taps of phase (py,px) of W[o,i,ky,kx] * x[i, a-(ky-py)/2, b-(kx-px)/2].
+// All 4 phases read x at one of 4 shifts {(0,0), (-1,0), (0,-1), (-1,-1)}; a workgroup owns a tile of
+// super-pixels (a,b) in [0,H]x[0,W] and all 4 phases, so every shifted input tile is staged ONCE and
+// feeds every phase that uses it (shift 0: 4 phases, shifts 1/2: 2, shift 3: 1 -> the 9 taps).
+// K steps are (channel chunk, shift); accumulators: 4 phases x TO x TM blocks (128 registers).
+
+struct ConvTParams {
+    const float* w[4][4];  // [shift][phase] -> [cin][cout] weight slice (nullptr: phase unused)
+};
+
+template <int S>
+struct ShiftPhases;  // phases (py*2+px) that read input shift S
+template <> struct ShiftPhases<0> { static constexpr int n = 4; static constexpr int p[4] = {0, 1, 2, 3}; };
+template <> struct ShiftPhases<1> { static constexpr int n = 2; static constexpr int p[4] = {0, 1, 0, 0}; };
+template <> struct ShiftPhases<2> { static constexpr int n = 2; static constexpr int p[4] = {0, 2, 0, 0}; };
+template <> struct ShiftPhases<3> { static constexpr int n = 1; static constexpr int p[4] = {0, 0, 0, 0}; };
+
+__host__ __device__ constexpr int shift_nph(int s) { return s == 0 ? 4 : (s == 3 ? 1 : 2); }
+
+template <int S, int TO, int TM, int BKT, int BO, int BM>
+__device__ __forceinline__ void convt_mma(const float* Ws, const float* Xs, int wo, int wm, int kh, int l32,
+                                          f32x16 (&acc)[4][TO][TM]) {
+    constexpr int NP = ShiftPhases<S>::n;
+#pragma unroll
+    for (int k0 = 0; k0 < BKT; k0 += 4) {
+        float af[2][NP][TO], bf[2][TM];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int kk = k0 + 2 * q + kh;
+#pragma unroll
+            for (int j = 0; j < TM; ++j) bf[q][j] = Xs[kk * BM + wm * TM * 32 + j * 32 + l32];
+#pragma unroll
+            for (int ph = 0; ph < NP; ++ph)
+#pragma unroll
+                for (int i = 0; i < TO; ++i) af[q][ph][i] = Ws[(ph * BKT + kk) * BO + wo * TO * 32 + i * 32 + l32];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int ph = 0; ph < NP; ++ph)
+#pragma unroll
+                for (int i = 0; i < TO; ++i)
+#pragma unroll
+                    for (int j = 0; j < TM; ++j)
+                        acc[ShiftPhases<S>::p[ph]][i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                            af[q][ph][i], bf[q][j], acc[ShiftPhases<S>::p[ph]][i][j], 0, 0, 0);
+    }
+}
+
+template <int WO, int WM, int TO, int TM, int BKT>
+__global__ __launch_bounds__(NT, 1) void convt_gemm_kernel(GemmParams p, ConvTParams q) {
+    static_assert(WO * WM == 4, "4 waves");
+    constexpr int BO = WO * TO * 32;
+    constexpr int BM = WM * TM * 32;
+    constexpr int XR = BKT * BM / NT;
+    constexpr int WV = BKT * BO / 4;         // float4 vectors per phase weight tile
+    constexpr int WPT = (WV + NT - 1) / NT;
+    constexpr int TILE = BKT * (4 * BO + BM);
+    static_assert(NT % BM == 0 && XR % 4 == 0, "thread->position map");
+    __shared__ float smem[2 * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wo = wave / WM, wm = wave % WM;
+    const int gh = p.in_h + 1, gw = p.in_w + 1, hw_g = gh * gw;
+    const int M = p.n * hw_g;
+    const int m0 = blockIdx.x * BM;
+    const int o0 = blockIdx.y * BO;
+    const int split = blockIdx.z;
+    const int cpk = p.cin / BKT;
+    const int ks_total = 4 * cpk;
+    const int ks_begin = (int)((int64_t)ks_total * split / p.nsplit);
+    const int ks_end = (int)((int64_t)ks_total * (split + 1) / p.nsplit);
+
+    const int ml = tid % BM, kr0 = (tid / BM) * XR;
+    const int m = m0 + ml;
+    const bool mvalid = m < M;
+    int nn = 0, a = 0, b = 0;
+    if (mvalid) {
+        nn = m / hw_g;
+        const int rem = m - nn * hw_g;
+        a = rem / gw;
+        b = rem - a * gw;
+    }
+    const int64_t in_hw = (int64_t)p.in_h * p.in_w;
+    const float* xbase = p.x + (int64_t)nn * p.cin * in_hw + (int64_t)kr0 * in_hw;
+    const bool has_s = p.s != nullptr;
+    const float* swhere = has_s ? p.s + (int64_t)nn * p.cin + kr0 : p.x;
+
+    float xr[XR];
+    float4 sr[XR / 4];
+    float4 wr[4][WPT];
+    bool xok = false;
+
+    auto load_step = [&](int ks) {
+        const int c = ks >> 2, sh = ks & 3;
+        const int ci0 = c * BKT;
+        const int iy = a - (sh & 1), ix = b - ((sh >> 1) & 1);
+        xok = mvalid && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w;
+        const float* src = xbase + (int64_t)ci0 * in_hw + (xok ? (int64_t)iy * p.in_w + ix : 0);
+#pragma unroll
+        for (int r = 0; r < XR; ++r) xr[r] = src[r * in_hw];
+#pragma unroll
+        for (int r = 0; r < XR; r += 4) sr[r / 4] = *reinterpret_cast<const float4*>(swhere + (has_s ? ci0 + r : 0));
+        const int nph = shift_nph(sh);
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+            if (ph >= nph) break;  // uniform
+            const int phase = sh == 0 ? ph : (sh == 1 ? (ph ? 1 : 0) : (sh == 2 ? (ph ? 2 : 0) : 0));
+            const float* wbase = q.w[sh][phase];
+#pragma unroll
+            for (int t = 0; t < WPT; ++t) {
+                int v = tid + t * NT;
+                v = v < WV ? v : v - WV;
+                const int wkk = v / (BO / 4), wc4 = v - wkk * (BO / 4);
+                const int o = o0 + wc4 * 4;
+                wr[ph][t] = *reinterpret_cast<const float4*>(wbase + (int64_t)(ci0 + wkk) * p.cout + (o < p.cout ? o : 0));
+            }
+        }
+    };
+    auto store_step = [&](int stage, int sh) {
+        float* Ws = smem + stage * TILE;
+        float* Xs = Ws + 4 * BKT * BO;
+#pragma unroll
+        for (int r = 0; r < XR; ++r) {
+            const float4 sv = sr[r / 4];
+            const float sc = has_s ? ((r & 3) == 0 ? sv.x : (r & 3) == 1 ? sv.y : (r & 3) == 2 ? sv.z : sv.w) : 1.f;
+            Xs[(kr0 + r) * BM + ml] = xok ? xr[r] * sc : 0.f;
+        }
+        const int nph = shift_nph(sh);
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+            if (ph >= nph) break;
+#pragma unroll
+            for (int t = 0; t < WPT; ++t) {
+                const int v = tid + t * NT;
+                const int wkk = v / (BO / 4), wc4 = v - wkk * (BO / 4);
+                float4 w = wr[ph][t];
+                if (o0 + wc4 * 4 >= p.cout) w = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (v < WV) *reinterpret_cast<float4*>(&Ws[(ph * BKT + wkk) * BO + wc4 * 4]) = w;
+            }
+        }
+    };
+
+    f32x16 acc[4][TO][TM];
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+        for (int i = 0; i < TO; ++i)
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[ph][i][j][r] = 0.f;
+
+    const int kh = lane >> 5, l32 = lane & 31;
+    int stage = 0;
+    if (ks_begin < ks_end) {
+        load_step(ks_begin);
+        store_step(0, ks_begin & 3);
+    }
+    __syncthreads();
+    for (int ks = ks_begin; ks < ks_end; ++ks) {
+        const bool more = ks + 1 < ks_end;
+        if (more) load_step(ks + 1);
+        const float* Ws = smem + stage * TILE;
+        const float* Xs = Ws + 4 * BKT * BO;
+        switch (ks & 3) {
+            case 0: convt_mma<0, TO, TM, BKT, BO, BM>(Ws, Xs, wo, wm, kh, l32, acc); break;
+            case 1: convt_mma<1, TO, TM, BKT, BO, BM>(Ws, Xs, wo, wm, kh, l32, acc); break;
+            case 2: convt_mma<2, TO, TM, BKT, BO, BM>(Ws, Xs, wo, wm, kh, l32, acc); break;
+            default: convt_mma<3, TO, TM, BKT, BO, BM>(Ws, Xs, wo, wm, kh, l32, acc); break;
+        }
+        if (more) store_step(stage ^ 1, (ks + 1) & 3);
+        __syncthreads();
+        stage ^= 1;
+    }
+
+    // epilogue: raw T (mode STORE) or this split's partial plane
+    float* dst = p.nsplit > 1 ? p.y + (int64_t)split * p.split_stride : p.y;
+    const int64_t plane = (int64_t)p.y_h * p.y_w;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+        const int mc = m0 + wm * TM * 32 + j * 32 + l32;
+        if (mc >= M) continue;
+        const int en = mc / hw_g;
+        const int erem = mc - en * hw_g;
+        const int ea = erem / gw;
+        const int eb = erem - ea * gw;
+#pragma unroll
+        for (int i = 0; i < TO; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = o0 + wo * TO * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                if (o >= p.cout) continue;
+                float* row0 = dst + ((int64_t)en * p.cout + o) * plane + (int64_t)(2 * ea) * p.y_w + 2 * eb;
+                row0[0] = acc[0][i][j][r];
+                if (eb < p.in_w) row0[1] = acc[1][i][j][r];
+                if (ea < p.in_h) {
+                    row0[p.y_w] = acc[2][i][j][r];
+                    if (eb < p.in_w) row0[p.y_w + 1] = acc[3][i][j][r];
+                }
+            }
+        }
+    }
+}
+
+// Does this 4-phase description match the polyphase stride-2 transposed 3x3 conv built by
+// stylemc_amd.modconv.PackedConv (phase index py*2+px, taps at shifts {0,-1}^2)?  Fills the table.
+bool convt_fusable(int cin, int cout, int in_h, int in_w, int y_h, int y_w, const smc_conv_phase* ph, int nph,
+                   const smc_conv_epilogue* epi, ConvTParams* q) {
+    if (nph != 4 || y_h != 2 * in_h + 1 || y_w != 2 * in_w + 1) return false;
+    if (epi && epi->mode != SMC_EPI_STORE) return false;
+    if (getenv("SMC_NO_CONVT_FUSION")) return false;
+    // measured (tools/bench_gemm.py): the fused kernel (1 wave/SIMD, 128 accumulators) wins only on the
+    // 32-channel 1024-px layer (51 vs 42 TF/s); the per-phase kernel is faster on every wider layer.
+    if (cout > 32 && !getenv("SMC_FORCE_CONVT_FUSION")) return false;
+    ConvTParams t{};
+    int count = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int py = k >> 1, px = k & 1;
+        const smc_conv_phase& f = ph[k];
+        if (f.in_stride != 1 || f.out_sy != 2 || f.out_sx != 2 || f.out_oy != py || f.out_ox != px) return false;
+        for (int tp = 0; tp < f.ntaps; ++tp) {
+            const int dy = f.tap_dy[tp], dx = f.tap_dx[tp];
+            if ((dy != 0 && dy != -1) || (dx != 0 && dx != -1)) return false;
+            const int s = (dy == -1 ? 1 : 0) + (dx == -1 ? 2 : 0);
+            if (t.w[s][k]) return false;
+            t.w[s][k] = f.wk + (int64_t)tp * cin * cout;
+            ++count;
+        }
+    }
+    if (count != 9) return false;
+    for (int s = 0; s < 4; ++s)
+        for (int k = 0; k < 4; ++k) {
+            const bool want = s == 0 || (s == 1 && (k == 0 || k == 1)) || (s == 2 && (k == 0 || k == 2)) || (s == 3 && k == 0);
+            if (want != (t.w[s][k] != nullptr)) return false;
+        }
+    if (q) *q = t;
+    return true;
+}
+
+struct ConvTCfg {
+    int bo, bm, id;
+};
+
+ConvTCfg convt_cfg(int cout) {
+    if (cout % 128 == 0) return {128, 64, 0};
+    if (cout % 64 == 0) return {64, 128, 1};
+    return {32, 256, 2};
+}
+
+int plan_split_convt(int n, int cin, int cout, int in_h, int in_w) {
+    const ConvTCfg c = convt_cfg(cout);
+    const int64_t M = (int64_t)n * (in_h + 1) * (in_w + 1);
+    const int64_t blocks = smc::ceil_div(M, c.bm) * smc::ceil_div(cout, c.bo);
+    const int ks = 4 * (cin / BK);
+    if (const char* f = getenv("SMC_FORCE_SPLIT")) {
+        int v = atoi(f);
+        if (v >= 1) return v < ks ? v : ks;
+    }
+    const int64_t target = 2LL * smc::device_cu_count();
+    if (blocks >= target) return 1;
+    int s = (int)smc::ceil_div(target, blocks > 0 ? blocks : 1);
+    int cap = ks / 4;
+    if (cap > 16) cap = 16;
+    if (s > cap) s = cap;
+    return s < 1 ? 1 : s;
+}
+
 struct Cfg {
     int bo, bm;
 };
@@ -310,7 +610,12 @@ SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, 
                                              int nphases) {
     Cfg c;
     if (pick_cfg(cout, &c) < 0 || cin % BK != 0 || nphases < 1 || nphases > 4 || !phases) return 0;
-    const int s = plan_split(n, cin, cout, phases, nphases, c);
+    int s;
+    if (nphases == 4 && y_h % 2 == 1 && y_w % 2 == 1 &&
+        convt_fusable(cin, cout, (y_h - 1) / 2, (y_w - 1) / 2, y_h, y_w, phases, nphases, nullptr, nullptr))
+        s = plan_split_convt(n, cin, cout, (y_h - 1) / 2, (y_w - 1) / 2);
+    else
+        s = plan_split(n, cin, cout, phases, nphases, c);
     return s > 1 ? (int64_t)s * n * cout * y_h * y_w * (int64_t)sizeof(float) : 0;
 }
 
@@ -322,7 +627,9 @@ SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w
     if (rc != SMC_OK) return rc;
     Cfg c;
     const int cfg = pick_cfg(cout, &c);
-    const int nsplit = plan_split(n, cin, cout, phases, nphases, c);
+    ConvTParams ctp{};
+    const bool fused_t = convt_fusable(cin, cout, in_h, in_w, y_h, y_w, phases, nphases, epi, &ctp);
+    const int nsplit = fused_t ? plan_split_convt(n, cin, cout, in_h, in_w) : plan_split(n, cin, cout, phases, nphases, c);
     const int64_t plane_elems = (int64_t)n * cout * y_h * y_w;
     if (nsplit > 1) {
         const int64_t need = nsplit * plane_elems * (int64_t)sizeof(float);
@@ -358,21 +665,35 @@ SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w
     p.split_stride = plane_elems;
 
     hipStream_t st = smc::as_stream(stream);
+    if (fused_t) {
+        const ConvTCfg tc = convt_cfg(cout);
+        const int64_t M = (int64_t)n * (in_h + 1) * (in_w + 1);
+        dim3 g((unsigned)smc::ceil_div(M, tc.bm), (unsigned)smc::ceil_div(cout, tc.bo), (unsigned)nsplit);
+        if (tc.id == 0) hipLaunchKernelGGL((convt_gemm_kernel<2, 2, 2, 1, 16>), g, dim3(NT), 0, st, p, ctp);
+        else if (tc.id == 1) hipLaunchKernelGGL((convt_gemm_kernel<1, 4, 2, 1, 16>), g, dim3(NT), 0, st, p, ctp);
+        else hipLaunchKernelGGL((convt_gemm_kernel<1, 4, 1, 2, 16>), g, dim3(NT), 0, st, p, ctp);
+        rc = smc::check_launch("smc_conv_gemm_f32 (fused transposed conv)");
+        if (rc != SMC_OK || nsplit == 1) return rc;
+        return smc_modconv_epilogue_f32(workspace, nsplit, plane_elems, y, n, cout, y_h, y_w, &e, stream);
+    }
     dim3 grid((unsigned)smc::ceil_div(max_m, c.bm), (unsigned)smc::ceil_div(cout, c.bo), (unsigned)(nphases * nsplit));
     // BK=32 halves the barriers per FLOP; it pays on the long-K 512-channel layers, BK=16 (more
     // workgroups per CU: 32-40 KB LDS vs 64-80 KB) on the high-resolution ones (tools/bench_gemm.py).
     bool k32 = cin % 32 == 0 && cin >= 512;
     if (const char* f = getenv("SMC_FORCE_BK")) k32 = k32 && atoi(f) != 16;  // A/B knob (tools/bench_gemm.py)
-    if (cfg == 0) {
-        if (k32) hipLaunchKernelGGL((conv_gemm_kernel<2, 2, 2, 2, 32>), grid, dim3(NT), 0, st, p);
-        else hipLaunchKernelGGL((conv_gemm_kernel<2, 2, 2, 2, 16>), grid, dim3(NT), 0, st, p);
-    } else if (cfg == 1) {
-        if (k32) hipLaunchKernelGGL((conv_gemm_kernel<1, 4, 2, 2, 32>), grid, dim3(NT), 0, st, p);
-        else hipLaunchKernelGGL((conv_gemm_kernel<1, 4, 2, 2, 16>), grid, dim3(NT), 0, st, p);
-    } else {
-        if (k32) hipLaunchKernelGGL((conv_gemm_kernel<1, 4, 1, 2, 32>), grid, dim3(NT), 0, st, p);
-        else hipLaunchKernelGGL((conv_gemm_kernel<1, 4, 1, 2, 16>), grid, dim3(NT), 0, st, p);
-    }
+    // raw buffer loads need the input to fit a 32-bit byte offset
+    const bool buf = (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31) && !getenv("SMC_NO_BUFFER_LOADS");
+#define SMC_LAUNCH(WO_, WM_, TO_, TM_)                                                                       \
+    do {                                                                                                   \
+        if (k32 && buf) hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 32, true>), grid, dim3(NT), 0, st, p);   \
+        else if (k32) hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 32, false>), grid, dim3(NT), 0, st, p);    \
+        else if (buf) hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 16, true>), grid, dim3(NT), 0, st, p);     \
+        else hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 16, false>), grid, dim3(NT), 0, st, p);             \
+    } while (0)
+    if (cfg == 0) SMC_LAUNCH(2, 2, 2, 2);
+    else if (cfg == 1) SMC_LAUNCH(1, 4, 2, 2);
+    else SMC_LAUNCH(1, 4, 1, 2);
+#undef SMC_LAUNCH
     rc = smc::check_launch("smc_conv_gemm_f32");
     if (rc != SMC_OK || nsplit == 1) return rc;
     return smc_modconv_epilogue_f32(workspace, nsplit, plane_elems, y, n, cout, y_h, y_w, &e, stream);

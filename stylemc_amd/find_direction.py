@@ -63,9 +63,11 @@ class DirectionFinder:
 
     def __init__(self, G, styles_array, clip_losses, id_loss, resolution=1024, batch_size=4, learning_rate=1.5,
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
-                 seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None):
+                 seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
+                 overlap=True):
         self.G = G
         self.synth_fn = synth_fn or utils.generate_image_rows   # (G, until_k, styles, shapes, noise, delta=)
+        self.overlap = overlap                                  # original-image branch on a second stream
         self.device = styles_array.device
         self.styles_array = styles_array
         self.clip_losses = clip_losses            # [(CLIPLoss, weight)], 'double' -> [(B/32, 1), (B/16, .5)]
@@ -98,16 +100,40 @@ class DirectionFinder:
         self.styles_direction.copy_(d)
         self.delta = d[:, S_TRAINABLE_SPACE_CHANNELS].clone()
 
-    def _local_terms(self, styles, denom):
-        """Sum-form loss of this rank's shard: every per-sample term / global batch size."""
-        T = S_TRAINABLE_SPACE_CHANNELS
-        d = self.delta.detach().clone().requires_grad_(True)
-        img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+    def _original_branch(self, styles):
+        """Everything that depends only on the original image (no gradient): its synthesis, its IR-SE50
+        features and its CLIP embeddings."""
         with torch.no_grad():
             orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
-        id_terms = self.id_loss.per_sample(img, orig)
-        src, tgt = unprocess(orig, self.mean, self.std), unprocess(img, self.mean, self.std)
-        clip_terms = sum(w * cl.per_sample(src, tgt) for cl, w in self.clip_losses)
+            y_feats = self.id_loss.target_feats(orig)
+            src = unprocess(orig, self.mean, self.std)
+            src_embs = [cl.encode_src(src) for cl, _ in self.clip_losses]
+        return y_feats, src_embs
+
+    def _local_terms(self, styles, denom):
+        """Sum-form loss of this rank's shard: every per-sample term / global batch size.
+
+        On the GPU the original-image branch runs on a second HIP stream, concurrently with the edited
+        image's synthesis (it shares no data with it), and joins before the losses.
+        """
+        T = S_TRAINABLE_SPACE_CHANNELS
+        d = self.delta.detach().clone().requires_grad_(True)
+        side = self._side_stream()
+        if side is not None:
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                y_feats, src_embs = self._original_branch(styles)
+            img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+            main.wait_stream(side)
+            for t in [y_feats] + src_embs:
+                t.record_stream(main)
+        else:
+            img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+            y_feats, src_embs = self._original_branch(styles)
+        id_terms = self.id_loss.per_sample_with(img, y_feats)
+        tgt = unprocess(img, self.mean, self.std)
+        clip_terms = sum(w * cl.per_sample_with(e, tgt) for (cl, w), e in zip(self.clip_losses, src_embs))
         sT = styles[:, T]
         l2_sum = ((sT + d) - sT).square().sum()
         id_part = self.coef["id"] * id_terms.sum() / denom
@@ -115,6 +141,13 @@ class DirectionFinder:
         l2_part = self.coef["l2"] * l2_sum / (denom * len(T) * 512)
         (g,) = torch.autograd.grad(id_part + clip_part + l2_part, d)
         return g, torch.stack([clip_part.detach(), id_part.detach(), torch.zeros_like(l2_part), l2_part.detach()])
+
+    def _side_stream(self):
+        if not (self.overlap and self.device.type == "cuda"):
+            return None
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
 
     def step(self):
         self.it += 1

@@ -31,11 +31,17 @@ class IDLoss(nn.Module):
         x = F.adaptive_avg_pool2d(x, (112, 112))
         return self.facenet(x)
 
+    @torch.no_grad()
+    def target_feats(self, y):
+        """Features of the original image (detached in the reference, id_loss.py:32)."""
+        return self.extract_feats(y)
+
+    def per_sample_with(self, y_hat, y_feats):
+        return 1 - (self.extract_feats(y_hat) * y_feats).sum(dim=1)
+
     def per_sample(self, y_hat, y):
         """(1 - <f(y_hat_i), f(y_i)>) for each i; y's features are detached."""
-        with torch.no_grad():
-            y_feats = self.extract_feats(y)
-        return 1 - (self.extract_feats(y_hat) * y_feats).sum(dim=1)
+        return self.per_sample_with(y_hat, self.target_feats(y))
 
     def forward(self, y_hat, y):
         return self.per_sample(y_hat, y).mean(), 0.0

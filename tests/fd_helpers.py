@@ -54,9 +54,14 @@ class OracleID(torch.nn.Module):
         super().__init__()
         self.inner = OL.IDLoss(facenet)
 
-    def per_sample(self, y_hat, y):
-        f = self.inner.extract_feats(y).detach()
+    def target_feats(self, y):
+        return self.inner.extract_feats(y).detach()
+
+    def per_sample_with(self, y_hat, f):
         return 1 - (self.inner.extract_feats(y_hat) * f).sum(1)
+
+    def per_sample(self, y_hat, y):
+        return self.per_sample_with(y_hat, self.target_feats(y))
 
 
 class OracleCLIP(torch.nn.Module):
@@ -64,10 +69,16 @@ class OracleCLIP(torch.nn.Module):
         super().__init__()
         self.inner = OL.CLIPLoss(visual, text)
 
-    def per_sample(self, src, tgt):
-        f = self.inner.visual(tgt) - self.inner.visual(src)
+    def encode_src(self, src):
+        return self.inner.visual(src).detach()
+
+    def per_sample_with(self, e, tgt):
+        f = self.inner.visual(tgt) - e
         f = f / f.norm(dim=1, keepdim=True)
         return 1 - torch.nn.functional.cosine_similarity(f, self.inner.text_features)
+
+    def per_sample(self, src, tgt):
+        return self.per_sample_with(self.encode_src(src), tgt)
 
 
 class TinyFace(torch.nn.Module):
