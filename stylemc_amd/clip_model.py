@@ -79,8 +79,18 @@ class VisionTransformer(nn.Module):
         self.ln_post = nn.LayerNorm(width)
         self.proj = nn.Parameter(scale * torch.randn(width, output_dim))
 
+    def patch_embed(self, x):
+        """conv1 with kernel == stride and no padding is a GEMM over non-overlapping patches:
+        [B, grid^2, 3*p*p] @ W^T.  (MIOpen's backward-data for the 32x32/s32 conv spends ~200 s
+        tuning on a fresh box per batch size; this form has no such cost.)"""
+        b, c, h, w = x.shape
+        p = self.conv1.kernel_size[0]
+        g_h, g_w = h // p, w // p
+        patches = x.reshape(b, c, g_h, p, g_w, p).permute(0, 2, 4, 1, 3, 5).reshape(b, g_h * g_w, c * p * p)
+        return patches @ self.conv1.weight.reshape(self.conv1.out_channels, -1).t()
+
     def forward(self, x):
-        x = self.conv1(x).flatten(2).transpose(1, 2)                      # [B, grid^2, width]
+        x = self.patch_embed(x)                                           # [B, grid^2, width]
         cls = self.class_embedding.to(x.dtype).expand(x.shape[0], 1, -1)
         x = torch.cat([cls, x], dim=1) + self.positional_embedding.to(x.dtype)
         x = self.transformer(self.ln_pre(x))

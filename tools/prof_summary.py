@@ -3,7 +3,7 @@
     python tools/prof_summary.py gpurun_out/prof1/run_kernel_stats.csv [--steps N] > profiles/rXX_summary.md
 
 Reports the top kernels and the aggregate of the conv_gemm_kernel family (all template
-instantiations), whose average launch duration bench.py's live HIP-event timing must match.
+instantiations, plus the phase-fused convt_gemm_kernel that bench.py's timer also wraps), whose average launch duration bench.py's live HIP-event timing must match.
 """
 import csv
 import sys
@@ -18,11 +18,11 @@ def main():
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     print(f"# rocprofv3 kernel stats: `{path}`\n")
     print(f"total GPU kernel time: {tot / 1e6:.2f} ms" + (f" over {steps} steps ({tot / 1e6 / steps:.2f} ms/step)" if steps else ""))
-    fam = [r for r in rows if "conv_gemm_kernel" in r["Name"]]
+    fam = [r for r in rows if "conv_gemm_kernel" in r["Name"] or "convt_gemm_kernel" in r["Name"]]
     ft = sum(float(r["TotalDurationNs"]) for r in fam)
     fc = sum(int(r["Calls"]) for r in fam)
     if fc:
-        print(f"\nconv_gemm_kernel family: {fc} launches, {ft / 1e6:.2f} ms, average {ft / fc / 1e3:.1f} us/launch, "
+        print(f"\nconv_gemm_kernel family (incl. convt_gemm_kernel): {fc} launches, {ft / 1e6:.2f} ms, average {ft / fc / 1e3:.1f} us/launch, "
               f"{100 * ft / tot:.1f}% of GPU time\n")
     print("| ms total | % | calls | avg us | kernel |\n|---:|---:|---:|---:|---|")
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:30]:
