@@ -164,6 +164,82 @@ int smc_torgb_fwd_f32(const float* x, const float* w, const float* s, const floa
 int smc_torgb_bwd_f32(const float* g, const float* y, const float* w, const float* s, float* dx, int n, int cin,
                       int cout, int h, int w_, float clamp, int scale, int accumulate, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * CLIP ViT image tower (replaces the third-party openai/CLIP VisionTransformer that the reference
+ * calls through CLIPLoss.encode_image, clip_loss.py:21,25-26; weights frozen -> data gradient only).
+ *
+ * smc_linear_f32: C[M][N] = epi(A[M][K] . B[K][N]) on fp32 MFMA (row-major, leading dimensions in
+ * floats; K % 32 == 0, N % 4 == 0, A and B 16-B aligned).  B is the frozen weight stored K-major
+ * (nn.Linear weight^T for a forward product, the weight itself for its data gradient).
+ * Epilogue order: + bias[n]; * act'(dact_pre[m][n]); pre_save = v, v = act(v); + residual[m][n]
+ * (residual may alias C).  Workspace: smc_linear_workspace_size() bytes (split-K partial tiles).
+ */
+#define SMC_LIN_ACT_NONE 0
+#define SMC_LIN_ACT_QUICKGELU 1 /* x * sigmoid(1.702 x), CLIP's QuickGELU */
+
+typedef struct {
+    const float* bias;      /* [N] or NULL                                                    */
+    const float* dact_pre;  /* multiply by QuickGELU'(dact_pre[m*ld_dact+n]) or NULL           */
+    int ld_dact;
+    int act;                /* SMC_LIN_ACT_*                                                   */
+    float* pre_save;        /* pre-activation store when act != NONE, may be NULL              */
+    int ld_pre;
+    const float* residual;  /* added last, may be NULL or alias C                              */
+    int ld_res;
+} smc_linear_epilogue;
+
+int64_t smc_linear_workspace_size(int M, int N, int K);
+int smc_linear_f32(const float* a, int lda, const float* b, int ldb, float* c, int ldc, int M, int N, int K,
+                   const smc_linear_epilogue* epi, float* workspace, int64_t workspace_bytes, void* stream);
+
+/* LayerNorm over the last dim (nn.LayerNorm: biased variance, y = (x-mean)*rstd*w + b), one row per
+ * wave; dim % 64 == 0, dim <= 1024.  mean/rstd [rows] may be NULL.  Row strides in floats. */
+int smc_layernorm_fwd_f32(const float* x, int64_t ldx, const float* w, const float* b, float* y, int64_t ldy,
+                          float* mean, float* rstd, int rows, int dim, float eps, void* stream);
+/* dx = LN'(dy) (+ dres if not NULL); dx may alias dres. */
+int smc_layernorm_bwd_f32(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* mean,
+                          const float* rstd, const float* w, const float* dres, int64_t ldres, float* dx,
+                          int64_t lddx, int rows, int dim, void* stream);
+
+/* Multi-head softmax attention over qkv [batch*tokens][3*heads*64] (q | k | v, nn.MultiheadAttention
+ * in_proj order) -> out [batch*tokens][heads*64]; p_save [batch][heads][tokens][tokens] may be NULL.
+ * head_dim must be 64.  The backward writes dqkv [batch*tokens][3*heads*64]. */
+int smc_attention_fwd_f32(const float* qkv, float* out, float* p_save, int batch, int tokens, int heads,
+                          int head_dim, float scale, void* stream);
+int smc_attention_bwd_f32(const float* dout, const float* qkv, const float* p_save, float* dqkv, int batch,
+                          int tokens, int heads, int head_dim, float scale, void* stream);
+
+/* Non-overlapping patch extraction (conv kernel == stride): img [batch][channels][grid*patch]^2 <->
+ * patches [batch*grid*grid][channels*patch*patch]; inverse = 1 writes img from patches. */
+int smc_patch_im2col_f32(const float* img, float* patches, int batch, int channels, int grid, int patch,
+                         int inverse, void* stream);
+
+typedef struct {
+    int width, layers, heads, patch, grid, out_dim, in_ch; /* ViT-B/32: 768, 12, 12, 32, 7, 512, 3 */
+    float ln_eps;                                          /* 1e-5 (nn.LayerNorm default)          */
+} smc_vit_config;
+
+/* Packed frozen weights: one fp32 buffer, segments in this order, each padded to 64 floats:
+ *   conv_wt [C*p*p][D], conv_w [D][C*p*p], class_embedding [D], positional_embedding [L][D],
+ *   ln_pre.{w,b} [D],
+ *   per layer: ln_1.{w,b}, in_proj_weight^T [D][3D], in_proj_weight [3D][D], in_proj_bias [3D],
+ *              out_proj.weight^T [D][D], out_proj.weight [D][D], out_proj.bias [D], ln_2.{w,b},
+ *              c_fc.weight^T [D][4D], c_fc.weight [4D][D], c_fc.bias [4D],
+ *              c_proj.weight^T [4D][D], c_proj.weight [D][4D], c_proj.bias [D],
+ *   ln_post.{w,b} [D], proj [D][E], proj^T [E][D]
+ * (the segment sizes of one layer are padded individually; see stylemc_amd/vit_hip.py). */
+int64_t smc_vit_packed_floats(const smc_vit_config* cfg);
+/* Activations the backward needs, per batch size (floats). */
+int64_t smc_vit_saved_floats(const smc_vit_config* cfg, int batch);
+int64_t smc_vit_workspace_bytes(const smc_vit_config* cfg, int batch);
+/* image [batch][in_ch][grid*patch][grid*patch] -> out [batch][out_dim]; saved may be NULL (no backward). */
+int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, const float* image, int batch, float* out,
+                        float* saved, float* workspace, int64_t workspace_bytes, void* stream);
+/* dimage = d out / d image applied to dout [batch][out_dim], from the forward's saved activations. */
+int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed, const float* dout, int batch,
+                         const float* saved, float* dimage, float* workspace, int64_t workspace_bytes,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

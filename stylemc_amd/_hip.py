@@ -32,6 +32,18 @@ class ConvEpilogue(ctypes.Structure):
                 ("gain", c_float), ("clamp", c_float), ("u_save", c_void_p)]
 
 
+class LinearEpilogue(ctypes.Structure):
+    _fields_ = [("bias", c_void_p), ("dact_pre", c_void_p), ("ld_dact", c_int), ("act", c_int),
+                ("pre_save", c_void_p), ("ld_pre", c_int), ("residual", c_void_p), ("ld_res", c_int)]
+
+
+class VitConfig(ctypes.Structure):
+    _fields_ = [("width", c_int), ("layers", c_int), ("heads", c_int), ("patch", c_int), ("grid", c_int),
+                ("out_dim", c_int), ("in_ch", c_int), ("ln_eps", c_float)]
+
+
+LIN_ACT_NONE, LIN_ACT_QUICKGELU = 0, 1
+
 P = c_void_p
 _SIGS = {
     "smc_abi_version": (c_int, []),
@@ -53,6 +65,18 @@ _SIGS = {
     "smc_modconv_demod_bwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, P]),
     "smc_torgb_fwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, P]),
     "smc_torgb_bwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, P]),
+    "smc_linear_workspace_size": (c_int64, [c_int, c_int, c_int]),
+    "smc_linear_f32": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P, P, c_int64, P]),
+    "smc_layernorm_fwd_f32": (c_int, [P, c_int64, P, P, P, c_int64, P, P, c_int, c_int, c_float, P]),
+    "smc_layernorm_bwd_f32": (c_int, [P, c_int64, P, c_int64, P, P, P, P, c_int64, P, c_int64, c_int, c_int, P]),
+    "smc_attention_fwd_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_float, P]),
+    "smc_attention_bwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, P]),
+    "smc_patch_im2col_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "smc_vit_packed_floats": (c_int64, [P]),
+    "smc_vit_saved_floats": (c_int64, [P, c_int]),
+    "smc_vit_workspace_bytes": (c_int64, [P, c_int]),
+    "smc_vit_forward_f32": (c_int, [P, P, P, c_int, P, P, P, c_int64, P]),
+    "smc_vit_backward_f32": (c_int, [P, P, P, c_int, P, P, P, c_int64, P]),
 }
 
 _lib = None

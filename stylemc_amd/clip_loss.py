@@ -2,24 +2,28 @@
 
 Without the third-party ``clip`` package and its weights (absent offline) the text direction is either
 given (``text_features``) or a seeded unit vector derived from the two prompts
-(``synthetic.text_direction``); the image tower is ``clip_model.VisionTransformer``.
+(``synthetic.text_direction``).  The image tower is ``vit_hip.HipVisionTransformer`` (``impl='hip'``,
+the default: the whole ViT on the gfx950 kernel library, BASELINE config 4) or
+``clip_model.VisionTransformer`` (``impl='torch'``: PyTorch-ROCm ops, BASELINE config 2).
 ``per_sample`` returns 1 - cos_i so the loss can be sharded over ranks and summed.
 """
 import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import clip_model, synthetic
+from . import clip_model, synthetic, vit_hip
 
 
 class CLIPLoss(nn.Module):
     def __init__(self, device="cuda", text_prompt="", negative_text_prompt="", clip_type="small", visual=None,
-                 text_features=None, visual_state_dict=None, seed=4):
+                 text_features=None, visual_state_dict=None, seed=4, impl="hip"):
         super().__init__()
         name = "ViT-B/32" if clip_type == "small" else "ViT-B/16"
         self.model_name = name
-        self.visual = visual if visual is not None else clip_model.build_visual(name, visual_state_dict, seed=seed,
-                                                                                device=device)
+        if impl not in ("hip", "torch"):
+            raise ValueError(f"impl must be 'hip' or 'torch', got {impl!r}")
+        builder = vit_hip.build_visual if impl == "hip" else clip_model.build_visual
+        self.visual = visual if visual is not None else builder(name, visual_state_dict, seed=seed, device=device)
         if text_features is None:
             text_features = synthetic.text_direction(text_prompt, negative_text_prompt)
         t = torch.as_tensor(text_features, dtype=torch.float32).reshape(1, -1).to(device)

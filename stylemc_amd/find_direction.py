@@ -206,14 +206,14 @@ def load_styles(s_input, n_seeds, device, seed=0):
     return synthetic.synthetic_styles(n_seeds, seed=seed).to(device)
 
 
-def build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip_loss_type="default"):
+def build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip_loss_type="default", impl="hip"):
     from .clip_loss import CLIPLoss
     if clip_loss_type != "default":
         raise NotImplementedError("the StyleGAN-NADA losses (clip_loss_nada.py) are outside the hot path")
     if clip_type == "double":
-        return [(CLIPLoss(device, text_prompt, negative_text_prompt, "small"), 1.0),
-                (CLIPLoss(device, text_prompt, negative_text_prompt, "large"), 0.5)]
-    return [(CLIPLoss(device, text_prompt, negative_text_prompt, clip_type), 1.0)]
+        return [(CLIPLoss(device, text_prompt, negative_text_prompt, "small", impl=impl), 1.0),
+                (CLIPLoss(device, text_prompt, negative_text_prompt, "large", impl=impl), 0.5)]
+    return [(CLIPLoss(device, text_prompt, negative_text_prompt, clip_type, impl=impl), 1.0)]
 
 
 def _cli():
