@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--clip-type", default="small")
     p.add_argument("--clip-impl", default="hip", choices=["hip", "torch"],
                    help="hip: ViT on the gfx950 kernel library (config 4); torch: PyTorch-ROCm ops (config 2)")
+    p.add_argument("--id-impl", default="hip", choices=["hip", "torch"],
+                   help="hip: IR-SE50 on the gfx950 kernel library (config 4); torch: PyTorch-ROCm/MIOpen (config 2)")
     p.add_argument("--cpu-iters", type=int, default=4)
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -123,7 +125,7 @@ def main():
     styles = synthetic.synthetic_styles(args.n_seeds, seed=0).to(dev)
     clip = build_clip_losses(args.clip_type, dev, "a photo of a face of a feminine woman with no makeup",
                              "a photo of a face of a masculine man", impl=args.clip_impl)
-    finder = DirectionFinder(G, styles, clip, IDLoss("a", device=dev, weights=None), resolution=args.resolution,
+    finder = DirectionFinder(G, styles, clip, IDLoss("a", device=dev, weights=None, impl=args.id_impl), resolution=args.resolution,
                              batch_size=args.batch, global_batch=args.batch * world.world_size, seed=0, world=world,
                              init_delta=initial_delta(0, 0.01), n_epochs=1000)
     for _ in range(args.warmup):
@@ -174,10 +176,10 @@ def main():
         "data": "synthetic (seeded config-f weights, S ~ N(1, 0.5) for 129 seeds, seeded CLIP/IR-SE50)",
         "config": {"workload": "find_direction step: 2x StyleGAN2 S-space synthesis fwd + 1 bwd (HIP), "
                                f"CLIP ViT-B/32 fwd/bwd ({'HIP' if args.clip_impl == 'hip' else 'PyTorch-ROCm'}), "
-                               "IR-SE50 fwd/bwd (PyTorch-ROCm), SGD",
+                               f"IR-SE50 fwd/bwd ({'HIP' if args.id_impl == 'hip' else 'PyTorch-ROCm'}), SGD",
                    "resolution": args.resolution, "batch_per_gpu": args.batch,
                    "global_batch": args.batch * world.world_size, "seeds_per_sec": round(seeds / dt, 3),
-                   "parallelism": f"dp{world.world_size}", "clip_type": args.clip_type, "clip_impl": args.clip_impl, "landmarks_loss_coef": 0,
+                   "parallelism": f"dp{world.world_size}", "clip_type": args.clip_type, "clip_impl": args.clip_impl, "id_impl": args.id_impl, "landmarks_loss_coef": 0,
                    "direction_finite": finite},
         "roofline": roofline,
         "cpu_baseline": None,

@@ -94,6 +94,10 @@ typedef struct {
 
 #define SMC_EPI_STORE 0   /* y = acc                                                           */
 #define SMC_EPI_MODACT 1  /* u = acc; y = clamp(act(u*d[n,o] + noise*strength + bias[o])*gain)  */
+/* modes of the IR-SE50 (ArcFace) convolutions, id_loss/model_irse.py:                           */
+#define SMC_EPI_PRELU 2      /* z = acc*scale_c[o] + bias[o]; u_save = z; y = z >= 0 ? z : alpha_c[o]*z */
+#define SMC_EPI_PRELU_GRAD 3 /* y = acc * (act_ref >= 0 ? 1 : alpha_c[o])  (PReLU backward)          */
+#define SMC_EPI_AFFINE 4     /* y = acc*scale_c[o] + bias[o]  (eval-mode BatchNorm)                  */
 
 typedef struct {
     int mode;                      /* SMC_EPI_*                                                  */
@@ -105,6 +109,11 @@ typedef struct {
     int act;                       /* SMC_ACT_* (linear / relu / lrelu on this path)               */
     float alpha, gain, clamp;      /* clamp < 0: none                                              */
     float* u_save;                 /* may be NULL: stores u (pre-demod acc), layout of y            */
+    const float* scale_c;          /* [cout] per-channel scale (multiplies d in MODACT), may be NULL */
+    const float* alpha_c;          /* [cout] PReLU slopes (PRELU / PRELU_GRAD)                      */
+    const float* act_ref;          /* PRELU_GRAD: the saved pre-activation, layout of y             */
+    const float* residual;         /* may be NULL: added last, [n][cout][y_h/rs][y_w/rs] at the      */
+    int residual_stride;           /*   positions with y % rs == 0 and x % rs == 0 (rs 0 -> 1)      */
 } smc_conv_epilogue;
 
 /* bytes of workspace smc_conv_gemm_f32 needs for these sizes (0 = none). */
@@ -239,6 +248,61 @@ int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, const fl
 int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed, const float* dout, int batch,
                          const float* saved, float* dimage, float* workspace, int64_t workspace_bytes,
                          void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * ArcFace IR-SE50 (id_loss/model_irse.py:10-49, helpers.py:56-119; run by IDLoss.extract_feats,
+ * id_loss/id_loss.py:20-24): forward and input gradient (frozen, eval-mode weights).
+ * The caller describes the network once (packed conv phases as for smc_conv_gemm_f32, eval-mode
+ * BatchNorms as per-channel scale a / shift b); see stylemc_amd/irse_hip.py for the packing.
+ */
+typedef struct {
+    int cin, depth, stride, in_h, in_w;  /* unit input [n][cin][in_h][in_w] -> [n][depth][in_h/s][in_w/s]   */
+    const float* bn1_a;                  /* [cin] res_layer BatchNorm2d (before conv1) as x*a + b              */
+    const float* bn1_b;
+    smc_conv_phase c1_fwd;               /* 3x3 stride 1, cin -> depth                                         */
+    smc_conv_phase c1_bwd;               /* its adjoint depth -> cin, bn1_a folded into the weights            */
+    const float* prelu;                  /* [depth]                                                            */
+    smc_conv_phase c2_fwd;               /* 3x3 stride s, depth -> depth                                       */
+    smc_conv_phase c2_bwd[4];            /* its adjoint (4 polyphase phases when s == 2), bn2_a folded         */
+    int c2_bwd_nphases;
+    const float* bn2_a;                  /* [depth]                                                            */
+    const float* bn2_b;
+    const float* se_w1;                  /* SE fc1 [hidden][depth]                                             */
+    const float* se_w2;                  /* SE fc2 [depth][hidden]                                             */
+    int se_hidden;
+    int sc_conv;                         /* shortcut: 0 = MaxPool2d(1, s) (cin == depth), 1 = conv1x1(s) + BN  */
+    smc_conv_phase sc_fwd;               /* 1 tap, in_stride s                                                 */
+    smc_conv_phase sc_bwd;               /* adjoint on the compact grid, sc_a folded                          */
+    const float* sc_a;
+    const float* sc_b;
+} smc_irse_unit;
+
+typedef struct {
+    int n_units;
+    const smc_irse_unit* units;
+    int in_h, in_w;                      /* 112 x 112                                                          */
+    int img_ch;                          /* 3                                                                  */
+    int stem_cin;                        /* img_ch padded to a multiple of 16 (zero channels / weights)        */
+    int stem_cout;                       /* 64                                                                 */
+    smc_conv_phase stem_fwd;             /* input_layer conv3x3                                                */
+    smc_conv_phase stem_bwd;             /* its adjoint, stem_bn_a folded                                      */
+    const float* stem_bn_a;
+    const float* stem_bn_b;
+    const float* stem_prelu;
+    int feat;                            /* 512                                                                */
+    int flat;                            /* 512*7*7                                                            */
+    const float* fc_wt;                  /* [flat][feat]: output BatchNorm2d + Linear + BatchNorm1d folded     */
+    const float* fc_w;                   /* [feat][flat] (data gradient)                                       */
+    const float* fc_b;                   /* [feat]                                                             */
+} smc_irse_net;
+
+int64_t smc_irse_saved_floats(const smc_irse_net* net, int n);
+int64_t smc_irse_workspace_bytes(const smc_irse_net* net, int n);
+/* img [n][img_ch][in_h][in_w] -> feat [n][feat] (before the l2 normalisation); saved may be NULL. */
+int smc_irse_forward_f32(const smc_irse_net* net, const float* img, int n, float* feat, float* saved,
+                         float* workspace, int64_t workspace_bytes, void* stream);
+int smc_irse_backward_f32(const smc_irse_net* net, const float* dfeat, int n, const float* saved, float* dimg,
+                          float* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

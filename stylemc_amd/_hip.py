@@ -17,7 +17,7 @@ c_int, c_int64, c_float, c_void_p, c_char_p = ctypes.c_int, ctypes.c_int64, ctyp
 
 ACT_CODES = {"linear": 1, "relu": 2, "lrelu": 3, "tanh": 4, "sigmoid": 5, "elu": 6, "selu": 7, "softplus": 8,
              "swish": 9}
-EPI_STORE, EPI_MODACT = 0, 1
+EPI_STORE, EPI_MODACT, EPI_PRELU, EPI_PRELU_GRAD, EPI_AFFINE = 0, 1, 2, 3, 4
 
 
 class ConvPhase(ctypes.Structure):
@@ -29,7 +29,8 @@ class ConvPhase(ctypes.Structure):
 class ConvEpilogue(ctypes.Structure):
     _fields_ = [("mode", c_int), ("d", c_void_p), ("noise", c_void_p), ("noise_nstride", c_int64),
                 ("noise_strength", c_void_p), ("bias", c_void_p), ("act", c_int), ("alpha", c_float),
-                ("gain", c_float), ("clamp", c_float), ("u_save", c_void_p)]
+                ("gain", c_float), ("clamp", c_float), ("u_save", c_void_p), ("scale_c", c_void_p),
+                ("alpha_c", c_void_p), ("act_ref", c_void_p), ("residual", c_void_p), ("residual_stride", c_int)]
 
 
 class LinearEpilogue(ctypes.Structure):
@@ -77,6 +78,10 @@ _SIGS = {
     "smc_vit_workspace_bytes": (c_int64, [P, c_int]),
     "smc_vit_forward_f32": (c_int, [P, P, P, c_int, P, P, P, c_int64, P]),
     "smc_vit_backward_f32": (c_int, [P, P, P, c_int, P, P, P, c_int64, P]),
+    "smc_irse_saved_floats": (c_int64, [P, c_int]),
+    "smc_irse_workspace_bytes": (c_int64, [P, c_int]),
+    "smc_irse_forward_f32": (c_int, [P, P, c_int, P, P, P, c_int64, P]),
+    "smc_irse_backward_f32": (c_int, [P, P, c_int, P, P, P, c_int64, P]),
 }
 
 _lib = None

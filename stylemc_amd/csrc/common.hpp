@@ -52,6 +52,45 @@ __device__ __forceinline__ float epi_y(float u, float d, float nz, float bias, i
     return clamp_fwd(act_fwd(act, z, alpha) * gain, clamp);
 }
 
+// Epilogue fields beyond the modconv ones (IR-SE50 modes, per-channel scale, strided residual).
+struct EpiExt {
+    const float* scale_c;
+    const float* alpha_c;
+    const float* act_ref;
+    const float* residual;
+    int rs;
+};
+
+inline EpiExt epi_ext(const smc_conv_epilogue* e) {
+    EpiExt x{};
+    x.rs = 1;
+    if (e) {
+        x.scale_c = e->scale_c; x.alpha_c = e->alpha_c; x.act_ref = e->act_ref; x.residual = e->residual;
+        x.rs = e->residual_stride > 0 ? e->residual_stride : 1;
+    }
+    return x;
+}
+
+// Modes PRELU / PRELU_GRAD / AFFINE and the residual (all modes) for output element idx = (n, o, yy, xx)
+// of a [.][cout][y_h][y_w] tensor.  MODACT's own math stays in epi_y (scale_c folded into its d).
+__device__ __forceinline__ float epi_ext_apply(int mode, float v, int n, int o, int64_t idx, int yy, int xx, int cout,
+                                               int y_h, int y_w, const float* bias, float* u_save, const EpiExt& x) {
+    if (mode == SMC_EPI_PRELU) {
+        const float z = v * (x.scale_c ? x.scale_c[o] : 1.f) + (bias ? bias[o] : 0.f);
+        if (u_save) u_save[idx] = z;
+        v = z >= 0.f ? z : z * x.alpha_c[o];
+    } else if (mode == SMC_EPI_PRELU_GRAD) {
+        v = x.act_ref[idx] >= 0.f ? v : v * x.alpha_c[o];
+    } else if (mode == SMC_EPI_AFFINE) {
+        v = v * (x.scale_c ? x.scale_c[o] : 1.f) + (bias ? bias[o] : 0.f);
+    }
+    if (x.residual && yy % x.rs == 0 && xx % x.rs == 0) {
+        const int rh = y_h / x.rs, rw = y_w / x.rs;
+        v += x.residual[(((int64_t)n * cout + o) * rh + yy / x.rs) * rw + xx / x.rs];
+    }
+    return v;
+}
+
 }  // namespace smc
 
 #define SMC_CHECK(cond, ...)                 \

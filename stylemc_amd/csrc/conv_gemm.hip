@@ -53,6 +53,7 @@ struct GemmParams {
     int act;
     float alpha, gain, clamp;
     float* u_save;
+    smc::EpiExt ext;
     int nsplit;
     int64_t split_stride;
 };
@@ -258,12 +259,18 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
                 if (o >= p.cout) continue;
                 const int64_t idx = ((int64_t)en * p.cout + o) * plane + pix;
                 const float v = acc[i][j][r];
-                if (p.nsplit > 1 || p.mode == SMC_EPI_STORE) {
+                if (p.nsplit > 1) {
                     dst[idx] = v;
-                } else {
+                } else if (p.mode == SMC_EPI_MODACT) {
                     if (p.u_save) p.u_save[idx] = v;
-                    dst[idx] = smc::epi_y(v, p.d ? p.d[(int64_t)en * p.cout + o] : 1.f, nz,
-                                          p.bias ? p.bias[o] : 0.f, p.act, p.alpha, p.gain, p.clamp);
+                    const float dd = (p.d ? p.d[(int64_t)en * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
+                    float r = smc::epi_y(v, dd, nz, p.bias ? p.bias[o] : 0.f, p.act, p.alpha, p.gain, p.clamp);
+                    if (p.ext.residual) r = smc::epi_ext_apply(SMC_EPI_STORE, r, en, o, idx, yy, xx, p.cout, p.y_h, p.y_w,
+                                                                nullptr, nullptr, p.ext);
+                    dst[idx] = r;
+                } else {
+                    dst[idx] = smc::epi_ext_apply(p.mode, v, en, o, idx, yy, xx, p.cout, p.y_h, p.y_w, p.bias, p.u_save,
+                                                  p.ext);
                 }
             }
         }
@@ -483,7 +490,7 @@ __global__ __launch_bounds__(NT, 1) void convt_gemm_kernel(GemmParams p, ConvTPa
 bool convt_fusable(int cin, int cout, int in_h, int in_w, int y_h, int y_w, const smc_conv_phase* ph, int nph,
                    const smc_conv_epilogue* epi, ConvTParams* q) {
     if (nph != 4 || y_h != 2 * in_h + 1 || y_w != 2 * in_w + 1) return false;
-    if (epi && epi->mode != SMC_EPI_STORE) return false;
+    if (epi && (epi->mode != SMC_EPI_STORE || epi->residual)) return false;
     if (getenv("SMC_NO_CONVT_FUSION")) return false;
     // measured (tools/bench_gemm.py): the fused kernel (1 wave/SIMD, 128 accumulators) wins only on the
     // 32-channel 1024-px layer (51 vs 42 TF/s); the per-phase kernel is faster on every wider layer.
@@ -661,6 +668,13 @@ SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w
     p.mode = e.mode; p.d = e.d; p.noise = e.noise; p.noise_nstride = e.noise_nstride;
     p.noise_strength = e.noise_strength; p.bias = e.bias; p.act = e.act; p.alpha = e.alpha; p.gain = e.gain;
     p.clamp = e.clamp; p.u_save = e.u_save;
+    p.ext = smc::epi_ext(epi);
+    if ((e.mode == SMC_EPI_PRELU || e.mode == SMC_EPI_PRELU_GRAD) && !e.alpha_c) {
+        smc::set_error("smc_conv_gemm_f32: PReLU epilogue needs alpha_c");
+        return SMC_ERR_INVALID;
+    }
+    SMC_CHECK(e.mode != SMC_EPI_PRELU_GRAD || e.act_ref, "smc_conv_gemm_f32: PRELU_GRAD needs act_ref");
+    SMC_CHECK(e.mode >= SMC_EPI_STORE && e.mode <= SMC_EPI_AFFINE, "smc_conv_gemm_f32: bad epilogue mode %d", e.mode);
     p.nsplit = nsplit;
     p.split_stride = plane_elems;
 

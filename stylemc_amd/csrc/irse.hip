@@ -1,0 +1,468 @@
+// ArcFace IR-SE50 (the identity-loss backbone) on gfx950: forward + data gradient, native executor.
+//
+// Replaces the PyTorch modules the reference runs in IDLoss.extract_feats (id_loss/id_loss.py:20-24,
+// id_loss/model_irse.py:10-49, id_loss/helpers.py:56-119).  Weights are frozen and eval-mode, so the
+// backward is the gradient w.r.t. the input face only.
+//
+// Every 3x3 / 1x1 convolution runs on the MFMA implicit-GEMM kernel (smc_conv_gemm_f32) with the
+// unit's elementwise work fused into its epilogue:
+//   stem   : y0 = PReLU(BN(conv3x3(x)))                 -> mode PRELU (BN as scale_c / bias), saves z
+//   unit   : y1 = PReLU(conv3x3(BN1(x)))                -> mode PRELU, saves the pre-activation u1
+//            r  = BN2(conv3x3_s(y1))                     -> mode AFFINE
+//            out = r * SE(r) + shortcut(x)               -> SE kernels + one combine pass, which also
+//                                                           writes BN1 of the next unit (xbn)
+//   output : BN2d -> flatten -> Linear -> BN1d           -> one GEMM (smc_linear_f32), all BNs folded
+// Backward: the conv adjoints are again gather GEMMs (stride-2 forward -> 4-phase polyphase adjoint),
+// with the BN scales folded into the packed adjoint weights, PReLU' fused as epilogue PRELU_GRAD, and
+// the shortcut gradient added by the conv1 adjoint's strided-residual epilogue.
+//
+// Layout: fp32 NCHW (the reference layout), batch-major; SE vectors [n][C].
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#include "common.hpp"
+
+namespace {
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+inline unsigned ew_grid(int64_t n) { return (unsigned)std::min<int64_t>(smc::ceil_div(n, 256), 16384); }
+
+// out[plane] = scale * sum_p a[plane][p] * (b ? b[plane][p] : 1): one wave per plane.
+__global__ __launch_bounds__(256) void plane_dot_kernel(const float* a, const float* b, float* out, int64_t planes,
+                                                        int hw, float scale) {
+    const int64_t pl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (pl >= planes) return;
+    const float* ap = a + pl * hw;
+    const float* bp = b ? b + pl * hw : nullptr;
+    float s = 0.f;
+    for (int i = lane; i < hw; i += 64) s += bp ? ap[i] * bp[i] : ap[i];
+    s = wsum(s);
+    if (lane == 0) out[pl] = s * scale;
+}
+
+// SE excitation per sample (one workgroup per n): h = relu(W1 m), g = sigmoid(W2 h).
+__global__ __launch_bounds__(256) void se_fwd_kernel(const float* m, const float* w1, const float* w2, float* h,
+                                                     float* g, int C, int hid) {
+    extern __shared__ float sm[];
+    float* ms = sm;
+    float* hs = sm + C;
+    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int c = tid; c < C; c += 256) ms[c] = m[(int64_t)n * C + c];
+    __syncthreads();
+    for (int j = wave; j < hid; j += 4) {
+        float s = 0.f;
+        for (int c = lane; c < C; c += 64) s += w1[(int64_t)j * C + c] * ms[c];
+        s = wsum(s);
+        if (lane == 0) {
+            const float v = s > 0.f ? s : 0.f;
+            hs[j] = v;
+            h[(int64_t)n * hid + j] = v;
+        }
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+        float s = 0.f;
+        for (int j = 0; j < hid; ++j) s += w2[(int64_t)c * hid + j] * hs[j];
+        g[(int64_t)n * C + c] = 1.f / (1.f + expf(-s));
+    }
+}
+
+// SE backward per sample: dz = dg * g(1-g); dh = (h > 0) * W2^T dz; dm = W1^T dh * inv_hw.
+__global__ __launch_bounds__(256) void se_bwd_kernel(const float* dg, const float* g, const float* h, const float* w1,
+                                                     const float* w2, float* dm, int C, int hid, float inv_hw) {
+    extern __shared__ float sm[];
+    float* dz = sm;
+    float* dh = sm + C;
+    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int c = tid; c < C; c += 256) {
+        const float gv = g[(int64_t)n * C + c];
+        dz[c] = dg[(int64_t)n * C + c] * gv * (1.f - gv);
+    }
+    __syncthreads();
+    for (int j = wave; j < hid; j += 4) {
+        float s = 0.f;
+        for (int c = lane; c < C; c += 64) s += w2[(int64_t)c * hid + j] * dz[c];
+        s = wsum(s);
+        if (lane == 0) dh[j] = h[(int64_t)n * hid + j] > 0.f ? s : 0.f;
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+        float s = 0.f;
+        for (int j = 0; j < hid; ++j) s += w1[(int64_t)j * C + c] * dh[j];
+        dm[(int64_t)n * C + c] = s * inv_hw;
+    }
+}
+
+// out = r * g[n,c] + shortcut; shortcut = sc[idx] (conv path) or x[n, c, s*y, s*x] (MaxPool2d(1, s));
+// xbn (optional) = out * a[c] + b[c]  (BN1 of the next unit).
+__global__ __launch_bounds__(256) void se_combine_kernel(const float* r, const float* g, const float* sc,
+                                                         const float* x, int s, int in_h, int in_w, float* out,
+                                                         float* xbn, const float* a, const float* b, int C, int oh,
+                                                         int ow, int64_t total) {
+    const int64_t ohw = (int64_t)oh * ow;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t nc = i / ohw;
+        const int p = (int)(i - nc * ohw);
+        float v = r[i] * g[nc];
+        if (sc) {
+            v += sc[i];
+        } else {
+            const int yy = p / ow, xx = p - yy * ow;
+            v += x[nc * ((int64_t)in_h * in_w) + (int64_t)(s * yy) * in_w + s * xx];
+        }
+        out[i] = v;
+        if (xbn) {
+            const int c = (int)(nc % C);
+            xbn[i] = v * a[c] + b[c];
+        }
+    }
+}
+
+// dr = dout * g[n,c] + dm[n,c]
+__global__ __launch_bounds__(256) void se_dr_kernel(const float* dout, const float* g, const float* dm, float* dr,
+                                                    int64_t hw, int64_t total) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t nc = i / hw;
+        dr[i] = dout[i] * g[nc] + dm[nc];
+    }
+}
+
+// y = x * a[c] + b[c]
+__global__ __launch_bounds__(256) void channel_affine_kernel(const float* x, const float* a, const float* b, float* y,
+                                                             int C, int64_t hw, int64_t total) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)((i / hw) % C);
+        y[i] = x[i] * a[c] + b[c];
+    }
+}
+
+// dz = dy * (z >= 0 ? 1 : alpha[c])
+__global__ __launch_bounds__(256) void prelu_grad_kernel(const float* dy, const float* z, const float* alpha, float* dz,
+                                                         int C, int64_t hw, int64_t total) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)((i / hw) % C);
+        dz[i] = z[i] >= 0.f ? dy[i] : dy[i] * alpha[c];
+    }
+}
+
+// Channel padding of the face [n][c_src][hw] <-> [n][c_dst][hw] (extra channels zero), either way.
+__global__ __launch_bounds__(256) void channel_copy_kernel(const float* src, int c_src, float* dst, int c_dst,
+                                                           int64_t hw, int64_t total /* n*c_dst*hw */) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t nc = i / hw;
+        const int64_t p = i - nc * hw;
+        const int c = (int)(nc % c_dst);
+        const int64_t n = nc / c_dst;
+        dst[i] = c < c_src ? src[(n * c_src + c) * hw + p] : 0.f;
+    }
+}
+
+// ------------------------------------------------------------------------------------------- executor
+
+inline int64_t rnd(int64_t n) { return (n + 63) & ~int64_t(63); }
+
+struct UnitS {
+    float *u1, *r, *h, *g;
+};
+
+int64_t unit_out_hw(const smc_irse_unit& u) { return (int64_t)(u.in_h / u.stride) * (u.in_w / u.stride); }
+
+int64_t saved_floats(const smc_irse_net& net, int n, float* base, UnitS* per_unit, float** stem_z) {
+    int64_t off = 0;
+    auto seg = [&](int64_t k) {
+        float* p = base ? base + off : nullptr;
+        off += rnd(k);
+        return p;
+    };
+    float* z = seg((int64_t)n * net.stem_cout * net.in_h * net.in_w);
+    if (stem_z) *stem_z = z;
+    for (int k = 0; k < net.n_units; ++k) {
+        const smc_irse_unit& u = net.units[k];
+        UnitS s;
+        s.u1 = seg((int64_t)n * u.depth * u.in_h * u.in_w);
+        s.r = seg((int64_t)n * u.depth * unit_out_hw(u));
+        s.h = seg((int64_t)n * u.se_hidden);
+        s.g = seg((int64_t)n * u.depth);
+        if (per_unit) per_unit[k] = s;
+    }
+    return off;
+}
+
+struct Ws {
+    float *pad, *xa, *xb, *xbn, *y1, *r, *sc, *m, *h, *g, *dm, *conv;
+    int64_t conv_bytes;
+};
+
+int64_t max_act(const smc_irse_net& net) {
+    int64_t m = (int64_t)net.stem_cout * net.in_h * net.in_w;
+    m = std::max(m, (int64_t)net.stem_cin * net.in_h * net.in_w);
+    for (int k = 0; k < net.n_units; ++k) {
+        const smc_irse_unit& u = net.units[k];
+        m = std::max(m, (int64_t)u.cin * u.in_h * u.in_w);
+        m = std::max(m, (int64_t)u.depth * u.in_h * u.in_w);
+    }
+    return m;
+}
+
+int max_channels(const smc_irse_net& net) {
+    int c = net.stem_cout;
+    for (int k = 0; k < net.n_units; ++k) c = std::max(c, net.units[k].depth);
+    return c;
+}
+
+int64_t conv_ws_need(const smc_irse_net& net, int n) {
+    int64_t m = 0;
+    auto q = [&](int cin, int cout, int yh, int yw, const smc_conv_phase* ph, int nph) {
+        m = std::max(m, smc_conv_gemm_workspace_size(n, cin, cout, yh, yw, ph, nph));
+    };
+    q(net.stem_cin, net.stem_cout, net.in_h, net.in_w, &net.stem_fwd, 1);
+    q(net.stem_cout, net.stem_cin, net.in_h, net.in_w, &net.stem_bwd, 1);
+    for (int k = 0; k < net.n_units; ++k) {
+        const smc_irse_unit& u = net.units[k];
+        const int oh = u.in_h / u.stride, ow = u.in_w / u.stride;
+        q(u.cin, u.depth, u.in_h, u.in_w, &u.c1_fwd, 1);
+        q(u.depth, u.cin, u.in_h, u.in_w, &u.c1_bwd, 1);
+        q(u.depth, u.depth, oh, ow, &u.c2_fwd, 1);
+        q(u.depth, u.depth, u.in_h, u.in_w, u.c2_bwd, u.c2_bwd_nphases);
+        if (u.sc_conv) {
+            q(u.cin, u.depth, oh, ow, &u.sc_fwd, 1);
+            q(u.depth, u.cin, oh, ow, &u.sc_bwd, 1);
+        }
+    }
+    const int64_t lin = std::max(smc_linear_workspace_size(n, net.feat, net.flat),
+                                 smc_linear_workspace_size(n, net.flat, net.feat));
+    return std::max(m, lin);
+}
+
+int64_t ws_floats(const smc_irse_net& net, int n, float* base, Ws* w) {
+    int64_t off = 0;
+    auto seg = [&](int64_t k) {
+        float* p = base ? base + off : nullptr;
+        off += rnd(k);
+        return p;
+    };
+    const int64_t act = (int64_t)n * max_act(net);
+    const int64_t vec = (int64_t)n * max_channels(net);
+    Ws t{};
+    t.pad = seg(act);
+    t.xa = seg(act);
+    t.xb = seg(act);
+    t.xbn = seg(act);
+    t.y1 = seg(act);
+    t.r = seg(act);
+    t.sc = seg(act);
+    t.m = seg(vec);
+    t.h = seg(vec);
+    t.g = seg(vec);
+    t.dm = seg(vec);
+    const int64_t cb = conv_ws_need(net, n);
+    t.conv = seg(smc::ceil_div(cb, 4) + 1);
+    t.conv_bytes = cb;
+    if (w) *w = t;
+    return off;
+}
+
+int net_validate(const smc_irse_net* net, int n) {
+    SMC_CHECK(net && net->units && net->n_units >= 1 && n >= 1, "smc_irse: bad net / batch");
+    SMC_CHECK(net->stem_cin >= net->img_ch && net->stem_cin % 16 == 0, "smc_irse: stem_cin must pad img_ch to 16k");
+    SMC_CHECK(net->fc_wt && net->fc_w && net->flat % 32 == 0 && net->feat % 32 == 0, "smc_irse: bad output layer");
+    for (int k = 0; k < net->n_units; ++k) {
+        const smc_irse_unit& u = net->units[k];
+        SMC_CHECK(u.stride == 1 || u.stride == 2, "smc_irse: unit %d stride %d", k, u.stride);
+        SMC_CHECK(u.in_h % u.stride == 0 && u.in_w % u.stride == 0, "smc_irse: unit %d odd size", k);
+        SMC_CHECK(u.se_hidden >= 1 && u.se_w1 && u.se_w2 && u.bn1_a && u.bn2_a && u.prelu, "smc_irse: unit %d", k);
+        SMC_CHECK(u.sc_conv || u.cin == u.depth, "smc_irse: unit %d identity shortcut needs cin == depth", k);
+        SMC_CHECK(u.c2_bwd_nphases == (u.stride == 2 ? 4 : 1), "smc_irse: unit %d adjoint phases", k);
+    }
+    const smc_irse_unit& last = net->units[net->n_units - 1];
+    SMC_CHECK((int64_t)last.depth * unit_out_hw(last) == net->flat, "smc_irse: flat %d mismatch", net->flat);
+    return SMC_OK;
+}
+
+smc_conv_epilogue epi_mode(int mode) {
+    smc_conv_epilogue e{};
+    e.mode = mode;
+    e.act = SMC_ACT_LINEAR;
+    e.gain = 1.f;
+    e.clamp = -1.f;
+    return e;
+}
+
+#define SMC_TRY(expr)                  \
+    do {                               \
+        const int rc_ = (expr);        \
+        if (rc_ != SMC_OK) return rc_; \
+    } while (0)
+
+}  // namespace
+
+SMC_API int64_t smc_irse_saved_floats(const smc_irse_net* net, int n) {
+    if (net_validate(net, n) != SMC_OK) return -1;
+    return saved_floats(*net, n, nullptr, nullptr, nullptr);
+}
+
+SMC_API int64_t smc_irse_workspace_bytes(const smc_irse_net* net, int n) {
+    if (net_validate(net, n) != SMC_OK) return -1;
+    return ws_floats(*net, n, nullptr, nullptr) * (int64_t)sizeof(float);
+}
+
+SMC_API int smc_irse_forward_f32(const smc_irse_net* net, const float* img, int n, float* feat, float* saved,
+                                 float* workspace, int64_t workspace_bytes, void* stream) {
+    SMC_TRY(net_validate(net, n));
+    SMC_CHECK(img && feat && workspace, "smc_irse_forward_f32: null pointer");
+    SMC_CHECK(workspace_bytes >= ws_floats(*net, n, nullptr, nullptr) * (int64_t)sizeof(float),
+              "smc_irse_forward_f32: workspace too small");
+    hipStream_t st = smc::as_stream(stream);
+    Ws w;
+    ws_floats(*net, n, workspace, &w);
+    std::vector<UnitS> us(net->n_units);
+    float* stem_z = nullptr;
+    if (saved) saved_floats(*net, n, saved, us.data(), &stem_z);
+    auto conv = [&](const float* x, int cin, int ih, int iw, float* y, int cout, int yh, int yw,
+                    const smc_conv_phase* ph, int nph, const smc_conv_epilogue& e) {
+        return smc_conv_gemm_f32(x, n, cin, ih, iw, y, cout, yh, yw, ph, nph, nullptr, &e, w.conv, w.conv_bytes,
+                                 stream);
+    };
+    const int H = net->in_h, W = net->in_w;
+    const int64_t hw0 = (int64_t)H * W;
+    // stem: pad the face to stem_cin channels, conv3x3 -> BN -> PReLU, then BN1 of unit 0
+    int64_t tot = (int64_t)n * net->stem_cin * hw0;
+    hipLaunchKernelGGL(channel_copy_kernel, dim3(ew_grid(tot)), dim3(256), 0, st, img, net->img_ch, w.pad,
+                       net->stem_cin, hw0, tot);
+    SMC_TRY(smc::check_launch("irse pad"));
+    smc_conv_epilogue e = epi_mode(SMC_EPI_PRELU);
+    e.scale_c = net->stem_bn_a;
+    e.bias = net->stem_bn_b;
+    e.alpha_c = net->stem_prelu;
+    e.u_save = stem_z;
+    float* x = w.xa;
+    SMC_TRY(conv(w.pad, net->stem_cin, H, W, x, net->stem_cout, H, W, &net->stem_fwd, 1, e));
+    tot = (int64_t)n * net->stem_cout * hw0;
+    hipLaunchKernelGGL(channel_affine_kernel, dim3(ew_grid(tot)), dim3(256), 0, st, x, net->units[0].bn1_a,
+                       net->units[0].bn1_b, w.xbn, net->stem_cout, hw0, tot);
+    SMC_TRY(smc::check_launch("irse bn1"));
+
+    for (int k = 0; k < net->n_units; ++k) {
+        const smc_irse_unit& u = net->units[k];
+        const int oh = u.in_h / u.stride, ow = u.in_w / u.stride;
+        const int64_t ohw = (int64_t)oh * ow;
+        float* r = saved ? us[k].r : w.r;
+        float* hbuf = saved ? us[k].h : w.h;
+        float* gbuf = saved ? us[k].g : w.g;
+        // y1 = PReLU(conv3x3(xbn))
+        e = epi_mode(SMC_EPI_PRELU);
+        e.alpha_c = u.prelu;
+        e.u_save = saved ? us[k].u1 : nullptr;
+        SMC_TRY(conv(w.xbn, u.cin, u.in_h, u.in_w, w.y1, u.depth, u.in_h, u.in_w, &u.c1_fwd, 1, e));
+        // r = BN2(conv3x3_s(y1))
+        e = epi_mode(SMC_EPI_AFFINE);
+        e.scale_c = u.bn2_a;
+        e.bias = u.bn2_b;
+        SMC_TRY(conv(w.y1, u.depth, u.in_h, u.in_w, r, u.depth, oh, ow, &u.c2_fwd, 1, e));
+        // SE: m = mean_hw(r); h = relu(W1 m); g = sigmoid(W2 h)
+        const int64_t planes = (int64_t)n * u.depth;
+        hipLaunchKernelGGL(plane_dot_kernel, dim3((unsigned)smc::ceil_div(planes, 4)), dim3(256), 0, st, r,
+                           (const float*)nullptr, w.m, planes, (int)ohw, 1.f / (float)ohw);
+        hipLaunchKernelGGL(se_fwd_kernel, dim3(n), dim3(256), sizeof(float) * (u.depth + u.se_hidden), st, w.m,
+                           u.se_w1, u.se_w2, hbuf, gbuf, u.depth, u.se_hidden);
+        SMC_TRY(smc::check_launch("irse se"));
+        // shortcut
+        const float* sc = nullptr;
+        if (u.sc_conv) {
+            e = epi_mode(SMC_EPI_AFFINE);
+            e.scale_c = u.sc_a;
+            e.bias = u.sc_b;
+            SMC_TRY(conv(x, u.cin, u.in_h, u.in_w, w.sc, u.depth, oh, ow, &u.sc_fwd, 1, e));
+            sc = w.sc;
+        }
+        // out = r * g + shortcut (+ BN1 of the next unit)
+        float* out = x == w.xa ? w.xb : w.xa;
+        const bool next = k + 1 < net->n_units;
+        tot = planes * ohw;
+        hipLaunchKernelGGL(se_combine_kernel, dim3(ew_grid(tot)), dim3(256), 0, st, r, gbuf, sc, x, u.stride,
+                           u.in_h, u.in_w, out, next ? w.xbn : nullptr, next ? net->units[k + 1].bn1_a : nullptr,
+                           next ? net->units[k + 1].bn1_b : nullptr, u.depth, oh, ow, tot);
+        SMC_TRY(smc::check_launch("irse combine"));
+        x = out;
+    }
+    // output layer: folded BN2d + Linear + BN1d
+    smc_linear_epilogue le{};
+    le.bias = net->fc_b;
+    return smc_linear_f32(x, net->flat, net->fc_wt, net->feat, feat, net->feat, n, net->feat, net->flat, &le, w.conv,
+                          w.conv_bytes, stream);
+}
+
+SMC_API int smc_irse_backward_f32(const smc_irse_net* net, const float* dfeat, int n, const float* saved, float* dimg,
+                                  float* workspace, int64_t workspace_bytes, void* stream) {
+    SMC_TRY(net_validate(net, n));
+    SMC_CHECK(dfeat && saved && dimg && workspace, "smc_irse_backward_f32: null pointer");
+    SMC_CHECK(workspace_bytes >= ws_floats(*net, n, nullptr, nullptr) * (int64_t)sizeof(float),
+              "smc_irse_backward_f32: workspace too small");
+    hipStream_t st = smc::as_stream(stream);
+    Ws w;
+    ws_floats(*net, n, workspace, &w);
+    std::vector<UnitS> us(net->n_units);
+    float* stem_z = nullptr;
+    saved_floats(*net, n, const_cast<float*>(saved), us.data(), &stem_z);
+    auto conv = [&](const float* x, int cin, int ih, int iw, float* y, int cout, int yh, int yw,
+                    const smc_conv_phase* ph, int nph, const smc_conv_epilogue& e) {
+        return smc_conv_gemm_f32(x, n, cin, ih, iw, y, cout, yh, yw, ph, nph, nullptr, &e, w.conv, w.conv_bytes,
+                                 stream);
+    };
+    // d(flattened last output) = dfeat @ fc_w
+    float* dx = w.xa;
+    SMC_TRY(smc_linear_f32(dfeat, net->feat, net->fc_w, net->flat, dx, net->flat, n, net->flat, net->feat, nullptr,
+                           w.conv, w.conv_bytes, stream));
+    for (int k = net->n_units - 1; k >= 0; --k) {
+        const smc_irse_unit& u = net->units[k];
+        const int oh = u.in_h / u.stride, ow = u.in_w / u.stride;
+        const int64_t ohw = (int64_t)oh * ow;
+        const int64_t planes = (int64_t)n * u.depth;
+        const float* dout = dx;
+        // SE + combine backward: dg = sum_hw dout * r; dm = SE chain; dr = dout * g + dm
+        hipLaunchKernelGGL(plane_dot_kernel, dim3((unsigned)smc::ceil_div(planes, 4)), dim3(256), 0, st, dout,
+                           us[k].r, w.m, planes, (int)ohw, 1.f);
+        hipLaunchKernelGGL(se_bwd_kernel, dim3(n), dim3(256), sizeof(float) * (u.depth + u.se_hidden), st, w.m,
+                           us[k].g, us[k].h, u.se_w1, u.se_w2, w.dm, u.depth, u.se_hidden, 1.f / (float)ohw);
+        const int64_t tot = planes * ohw;
+        hipLaunchKernelGGL(se_dr_kernel, dim3(ew_grid(tot)), dim3(256), 0, st, dout, us[k].g, w.dm, w.r, ohw, tot);
+        SMC_TRY(smc::check_launch("irse se bwd"));
+        // du1 = PReLU'(u1) * conv2^T(dr)   (BN2 scale folded into the adjoint weights)
+        smc_conv_epilogue e = epi_mode(SMC_EPI_PRELU_GRAD);
+        e.alpha_c = u.prelu;
+        e.act_ref = us[k].u1;
+        SMC_TRY(conv(w.r, u.depth, oh, ow, w.y1, u.depth, u.in_h, u.in_w, u.c2_bwd, u.c2_bwd_nphases, e));
+        // shortcut gradient: dout itself (MaxPool2d(1, s)) or the 1x1 conv adjoint (compact grid)
+        const float* res = dout;
+        if (u.sc_conv) {
+            SMC_TRY(conv(dout, u.depth, oh, ow, w.sc, u.cin, oh, ow, &u.sc_bwd, 1, epi_mode(SMC_EPI_STORE)));
+            res = w.sc;
+        }
+        // dx = conv1^T(du1) (BN1 scale folded) + shortcut gradient scattered at stride s
+        float* dnew = dx == w.xa ? w.xb : w.xa;
+        e = epi_mode(SMC_EPI_STORE);
+        e.residual = res;
+        e.residual_stride = u.stride;
+        SMC_TRY(conv(w.y1, u.depth, u.in_h, u.in_w, dnew, u.cin, u.in_h, u.in_w, &u.c1_bwd, 1, e));
+        dx = dnew;
+    }
+    // stem: dz = dy0 * PReLU'(z); d(padded face) = conv^T(dz) (BN scale folded); drop the pad channels
+    const int H = net->in_h, W = net->in_w;
+    const int64_t hw0 = (int64_t)H * W;
+    int64_t tot = (int64_t)n * net->stem_cout * hw0;
+    hipLaunchKernelGGL(prelu_grad_kernel, dim3(ew_grid(tot)), dim3(256), 0, st, dx, stem_z, net->stem_prelu, w.y1,
+                       net->stem_cout, hw0, tot);
+    SMC_TRY(smc::check_launch("irse stem prelu'"));
+    SMC_TRY(conv(w.y1, net->stem_cout, H, W, w.pad, net->stem_cin, H, W, &net->stem_bwd, 1, epi_mode(SMC_EPI_STORE)));
+    tot = (int64_t)n * net->img_ch * hw0;
+    hipLaunchKernelGGL(channel_copy_kernel, dim3(ew_grid(tot)), dim3(256), 0, st, w.pad, net->stem_cin, dimg,
+                       net->img_ch, hw0, tot);
+    return smc::check_launch("irse unpad");
+}

@@ -22,6 +22,7 @@ struct Epi {
     int act;
     float alpha, gain, clamp;
     float* u_save;
+    smc::EpiExt ext;
 };
 
 Epi to_epi(const smc_conv_epilogue* e) {
@@ -35,6 +36,7 @@ Epi to_epi(const smc_conv_epilogue* e) {
         r.noise_strength = e->noise_strength; r.bias = e->bias; r.act = e->act; r.alpha = e->alpha;
         r.gain = e->gain; r.clamp = e->clamp; r.u_save = e->u_save;
     }
+    r.ext = smc::epi_ext(e);
     return r;
 }
 
@@ -57,22 +59,31 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
 // ---------------------------------------------------------------------------------------------- epilogue
 
 __global__ __launch_bounds__(256) void epilogue_kernel(const float* src, int nsplit, int64_t split_stride, float* y,
-                                                       int c, int64_t hw, int64_t total, Epi e) {
+                                                       int c, int h, int w, int64_t total, Epi e) {
     const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t hw = (int64_t)h * w;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
         float v = src[idx];
         for (int s = 1; s < nsplit; ++s) v += src[s * split_stride + idx];
-        if (e.mode == SMC_EPI_STORE) {
+        if (e.mode == SMC_EPI_STORE && !e.ext.residual) {
             y[idx] = v;
             continue;
         }
         const int64_t nc = idx / hw;
         const int64_t pix = idx - nc * hw;
         const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
-        if (e.u_save) e.u_save[idx] = v;
-        const float nz = e.noise ? e.noise[n * e.noise_nstride + pix] * nstr : 0.f;
-        y[idx] = smc::epi_y(v, e.d ? e.d[nc] : 1.f, nz, e.bias ? e.bias[o] : 0.f, e.act, e.alpha, e.gain, e.clamp);
+        const int yy = (int)(pix / w), xx = (int)(pix - (int64_t)yy * w);
+        if (e.mode == SMC_EPI_MODACT) {
+            if (e.u_save) e.u_save[idx] = v;
+            const float nz = e.noise ? e.noise[n * e.noise_nstride + pix] * nstr : 0.f;
+            const float dd = (e.d ? e.d[nc] : 1.f) * (e.ext.scale_c ? e.ext.scale_c[o] : 1.f);
+            float r = smc::epi_y(v, dd, nz, e.bias ? e.bias[o] : 0.f, e.act, e.alpha, e.gain, e.clamp);
+            if (e.ext.residual) r = smc::epi_ext_apply(SMC_EPI_STORE, r, n, o, idx, yy, xx, c, h, w, nullptr, nullptr, e.ext);
+            y[idx] = r;
+        } else {
+            y[idx] = smc::epi_ext_apply(e.mode, v, n, o, idx, yy, xx, c, h, w, e.bias, e.u_save, e.ext);
+        }
     }
 }
 
@@ -392,7 +403,7 @@ SMC_API int smc_modconv_epilogue_f32(const float* src, int nsplit, int64_t split
     SMC_CHECK(src && y && n >= 1 && c >= 1 && h >= 1 && w >= 1 && nsplit >= 1, "smc_modconv_epilogue_f32: bad args");
     const int64_t total = (int64_t)n * c * h * w;
     hipLaunchKernelGGL(epilogue_kernel, dim3((unsigned)grid_cap(smc::ceil_div(total, 256))), dim3(256), 0,
-                       smc::as_stream(stream), src, nsplit, split_stride, y, c, (int64_t)h * w, total, to_epi(epi));
+                       smc::as_stream(stream), src, nsplit, split_stride, y, c, h, w, total, to_epi(epi));
     return smc::check_launch("smc_modconv_epilogue_f32");
 }
 

@@ -1,7 +1,8 @@
 """Identity loss (id_loss/id_loss.py:7-39): 1 - <ArcFace(y_hat), ArcFace(y).detach()>, batch mean.
 
 ``extract_feats``: adaptive-avg-pool to 256 (4x4 mean at 1024 px), crop [35:223, 32:220], adaptive pool
-to 112, IR-SE50, l2-normalised.  The target image's features are computed under no_grad (the reference detaches them, :32), so the
+to 112, IR-SE50, l2-normalised.  IR-SE50 runs on the gfx950 kernel library (``impl='hip'``, default:
+stylemc_amd.irse_hip, BASELINE config 4) or on PyTorch-ROCm/MIOpen (``impl='torch'``, config 2).  The target image's features are computed under no_grad (the reference detaches them, :32), so the
 backbone backward runs for y_hat only; the per-sample dot loop (id_loss.py:34-37) is a batched row dot.
 """
 import os
@@ -14,13 +15,20 @@ from .model_irse import build_irse50
 
 
 class IDLoss(nn.Module):
-    def __init__(self, opts=None, facenet=None, weights="id_loss/model_ir_se50.pth", device="cuda", seed=3):
+    def __init__(self, opts=None, facenet=None, weights="id_loss/model_ir_se50.pth", device="cuda", seed=3,
+                 impl="hip"):
         super().__init__()
         if facenet is None:
             sd = None
             if weights and os.path.exists(weights):
                 sd = torch.load(weights, map_location="cpu", weights_only=True)
-            facenet = build_irse50(sd, seed=seed, device=device)
+            if impl == "hip":
+                from ..irse_hip import build_irse50 as build_hip
+                facenet = build_hip(sd, seed=seed, device=device)
+            elif impl == "torch":
+                facenet = build_irse50(sd, seed=seed, device=device)
+            else:
+                raise ValueError(f"impl must be 'hip' or 'torch', got {impl!r}")
         self.facenet = facenet.eval()
         self.opts = opts
 

@@ -1,4 +1,4 @@
-"""Host-side checks of the HIP ViT drop-in (no GPU): the packed weight layout agrees with the library's,
+"""Host-side checks of the HIP ViT and IR-SE50 drop-ins (no GPU): the packed weight layout agrees with the library's,
 the state_dict keeps the openai/CLIP ``visual.*`` keys, and CPU tensors are refused (no CPU fallback)."""
 import ctypes
 
@@ -39,3 +39,20 @@ def test_unsupported_config_and_cpu_refused():
     m.refresh()
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 3, 64, 64))
+
+
+def test_irse50_descriptor_builds_on_host():
+    """IR-SE50 packing (BN folds, adjoint phases) builds without a GPU; the library accepts the net."""
+    from stylemc_amd import irse_hip
+    net = irse_hip.HipIRSE50()
+    pk = net.packed_net()
+    assert pk.net.n_units == 24 and pk.net.flat == 512 * 7 * 7 and pk.net.stem_cin == 16
+    strides = [pk.units[k].stride for k in range(24)]
+    assert strides == [2, 1, 1, 2, 1, 1, 1, 2] + [1] * 13 + [2, 1, 1]
+    assert all(pk.units[k].c2_bwd_nphases == (4 if strides[k] == 2 else 1) for k in range(24))
+    assert [pk.units[k].sc_conv for k in (0, 3, 7, 21)] == [0, 1, 1, 1]
+    lib = _hip.load()
+    assert lib.smc_irse_saved_floats(ctypes.byref(pk.net), 4) > 0
+    assert lib.smc_irse_workspace_bytes(ctypes.byref(pk.net), 4) > 0
+    with pytest.raises(RuntimeError):
+        net(torch.zeros(1, 3, 112, 112))
