@@ -13,11 +13,15 @@ all_reduce of the direction gradient per step).  value = images/s = 2 x seeds/s 
 image per seed), seeds counted exactly (the batch picker can draw the short
 last batch of the 129 seeds).
 
-roofline: the dominant kernel family, ``conv_gemm_kernel`` (the MFMA implicit-GEMM modulated conv,
-all template instantiations): algorithmic FLOPs of each launch (dense MACs x 2 of the conv it
-computes) / its duration, timed with HIP events around every launch in the
-timed region, against the fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).  traffic: HBM
-bytes per launch from the rocprofv3 PMC pass recorded in profiles/pmc_traffic.json (null if absent).
+roofline: the dominant kernel family, the synthesis modconv GEMMs (``conv_gemm_lds_kernel`` /
+``conv_gemm_kernel`` / ``convt_gemm_kernel``, every launch of smc_conv_gemm_f32 from modconv.py):
+algorithmic FLOPs of each launch (dense MACs x 2 of the conv it computes) / its
+duration, timed with HIP events around every launch during --roofline-steps extra steps run right
+after the timed region with the original-image branch serialised onto the main stream (in the timed
+region that branch runs on a second stream, and a launch's event interval would include CU time
+taken by the other stream's kernels), against the fp32 MFMA peak (157.3 TFLOP/s,
+MI355X_MICROARCH.md).  traffic: HBM bytes per launch from the rocprofv3 PMC pass recorded in
+profiles/pmc_traffic.json (null if absent).
 
 cpu_baseline (rank 0, N=1): the test oracle (pure-torch fp32 CPU restatement of the reference
 algorithm, oracle/) running the same step at FFHQ-1024 with batch 1 for --cpu-iters iterations on
@@ -54,7 +58,8 @@ def parse():
     p.add_argument("--cpu-iters", type=int, default=4)
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-kernel-timer", action="store_true", help="skip the per-launch HIP events")
+    p.add_argument("--no-kernel-timer", action="store_true", help="skip the roofline pass")
+    p.add_argument("--roofline-steps", type=int, default=2, help="serialised steps timed per launch for the roofline")
     return p.parse_args()
 
 
@@ -133,8 +138,7 @@ def main():
     torch.cuda.synchronize()
     world.barrier()
 
-    timer = None if args.no_kernel_timer else _hip.KernelTimer("conv_gemm")
-    _hip.set_timer(timer)
+    # timed region: throughput (no per-launch events in it)
     seeds = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -144,20 +148,35 @@ def main():
     torch.cuda.synchronize()
     world.barrier()
     dt = time.perf_counter() - t0
-    _hip.set_timer(None)
     dt = world.all_max(dt, dev)
     finite = bool(torch.isfinite(finder.delta).all().item())
 
+    # roofline pass: the same step with the original-image branch serialised onto the main stream, so
+    # each GEMM launch's HIP-event duration is its own execution time (with the side stream running
+    # concurrently the events would also count CU time taken by the other stream's kernels; rocprofv3's
+    # kernel trace, profiles/, measures the serialised duration too)
     roofline = None
-    if timer is not None:
+    if not args.no_kernel_timer and args.roofline_steps > 0:
+        timer = _hip.KernelTimer("conv_gemm")
+        finder.overlap = False
+        _hip.set_timer(timer)
+        t1 = time.perf_counter()
+        for _ in range(args.roofline_steps):
+            finder.step()
+        torch.cuda.synchronize()
+        dt_r = time.perf_counter() - t1
+        _hip.set_timer(None)
+        finder.overlap = True
         s = timer.summary()
         achieved = s["flops"] / s["seconds"] / 1e12 if s["seconds"] > 0 else 0.0
         roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),
-                    "kernel": "conv_gemm_kernel (all instantiations)", "launches": s["launches"],
+                    "kernel": "conv_gemm_kernel family (synthesis modconv GEMMs)", "launches": s["launches"],
                     "avg_launch_us": round(1e6 * s["seconds"] / max(s["launches"], 1), 2),
                     "alg_gflop_per_launch": round(s["flops"] / max(s["launches"], 1) / 1e9, 3),
-                    "share_of_step_time": round(s["seconds"] / dt, 4)}
+                    "share_of_step_time": round(s["seconds"] / dt_r, 4),
+                    "measured": f"HIP events around every launch, {args.roofline_steps} serialised steps after the "
+                                f"timed region"}
 
     if world.rank != 0:
         return

@@ -11,6 +11,10 @@
 namespace smc {
 
 void set_error(const char* fmt, ...);
+// smc_conv_gemm_f32 under the IR-SE50 executor's kernel names (TAG 1; conv_gemm.hip)
+int conv_gemm_aux(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h, int y_w,
+                  const smc_conv_phase* phases, int nphases, const float* s_in, const smc_conv_epilogue* epi,
+                  float* workspace, int64_t workspace_bytes, void* stream);
 int check_launch(const char* what);
 int device_cu_count();
 

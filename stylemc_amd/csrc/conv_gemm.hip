@@ -17,6 +17,7 @@
 // are prefetched into registers while the MFMAs consume the LDS copy (register staging, one LDS
 // buffer, two barriers per step).  Low-parallelism shapes (the 4..16 px blocks) split K across
 // workgroups into a workspace that the epilogue kernel reduces.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -34,6 +35,7 @@ struct PhaseDev {
     int in_stride;
     int out_h, out_w, out_oy, out_ox, out_sy, out_sx;
     const float* wk;
+    int64_t wstride;  // LDS-DMA kernel: floats between two samples' weights (0 = shared weights)
 };
 
 struct GemmParams {
@@ -58,7 +60,56 @@ struct GemmParams {
     int64_t split_stride;
 };
 
-template <int WO, int WM, int TO, int TM, int BKT, bool BUF>
+// Epilogue shared by the gather-GEMM kernels: lane owns column m, registers walk output channels.
+template <int WO, int WM, int TO, int TM>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const PhaseDev& ph, const f32x16 (&acc)[TO][TM],
+                                              int m0, int o0, int M, int hw_out, int split, int wo, int wm, int kh,
+                                              int l32) {
+    const float nstr = p.noise_strength ? *p.noise_strength : 1.f;
+    float* dst = p.nsplit > 1 ? p.y + (int64_t)split * p.split_stride : p.y;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+        const int mc = m0 + wm * TM * 32 + j * 32 + l32;
+        if (mc >= M) continue;
+        const int en = mc / hw_out;
+        const int erem = mc - en * hw_out;
+        const int ea = erem / ph.out_w;
+        const int eb = erem - ea * ph.out_w;
+        const int yy = ph.out_oy + ph.out_sy * ea;
+        const int xx = ph.out_ox + ph.out_sx * eb;
+        const int64_t pix = (int64_t)yy * p.y_w + xx;
+        const int64_t plane = (int64_t)p.y_h * p.y_w;
+        float nz = 0.f;
+        if (p.nsplit == 1 && p.mode == SMC_EPI_MODACT && p.noise) nz = p.noise[en * p.noise_nstride + pix] * nstr;
+#pragma unroll
+        for (int i = 0; i < TO; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = o0 + wo * TO * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                if (o >= p.cout) continue;
+                const int64_t idx = ((int64_t)en * p.cout + o) * plane + pix;
+                const float v = acc[i][j][r];
+                if (p.nsplit > 1) {
+                    dst[idx] = v;
+                } else if (p.mode == SMC_EPI_MODACT) {
+                    if (p.u_save) p.u_save[idx] = v;
+                    const float dd = (p.d ? p.d[(int64_t)en * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
+                    float q = smc::epi_y(v, dd, nz, p.bias ? p.bias[o] : 0.f, p.act, p.alpha, p.gain, p.clamp);
+                    if (p.ext.residual) q = smc::epi_ext_apply(SMC_EPI_STORE, q, en, o, idx, yy, xx, p.cout, p.y_h, p.y_w,
+                                                                nullptr, nullptr, p.ext);
+                    dst[idx] = q;
+                } else {
+                    dst[idx] = smc::epi_ext_apply(p.mode, v, en, o, idx, yy, xx, p.cout, p.y_h, p.y_w, p.bias, p.u_save,
+                                                  p.ext);
+                }
+            }
+        }
+    }
+}
+
+// TAG only renames the instantiation (0: the synthesis modconv, 1: the IR-SE50 executor), so profiles can
+// tell the two GEMM families apart.
+template <int WO, int WM, int TO, int TM, int BKT, bool BUF, int TAG = 0>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
     static_assert(WO * WM == 4, "4 waves");
     constexpr int BO = WO * TO * 32;
@@ -234,46 +285,190 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
         stage ^= 1;
     }
 
-    // ---- epilogue: lane owns column m, registers walk output channels
-    const float nstr = p.noise_strength ? *p.noise_strength : 1.f;
-    float* dst = p.nsplit > 1 ? p.y + (int64_t)split * p.split_stride : p.y;
+    gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// LDS-DMA variant (the default where it applies): both operand tiles go global -> LDS with no VGPR
+// staging -- the input slab by `buffer_load_dword ... lds` (lane = position, 4 B, the buffer range check
+// zero-fills out-of-image taps), the weight slab by `global_load_lds_dword[x4]` -- into an NST-deep LDS
+// ring.  Loads run NST-1 K steps ahead; each step waits with a counted vmcnt (never 0 in steady state)
+// and a raw s_barrier (a __syncthreads would drain the in-flight DMA, cdna_hip_programming.md section 5
+// "Pipelining across barriers").  Nothing is transformed in transit, so the style scale s[n,i] lives in
+// per-sample weights W[t][i][o]*s[n,i] prepared by wscale_kernel (a workgroup's positions lie in one
+// image); s == NULL (data gradients, IR-SE50) reads the shared weights.
+
+template <int WF>
+struct WeightDma {
+    static constexpr int ww = WF % 1024 == 0 ? 4 : 1;  // floats per lane of one weight DMA
+    static constexpr int bytes = ww * 4;
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int WO, int WM, int TO, int TM, int BKT, int NST, int TAG = 0>
+__global__ __launch_bounds__(NT, 2) void conv_gemm_lds_kernel(GemmParams p) {
+    static_assert(WO * WM == 4, "4 waves");
+    constexpr int BO = WO * TO * 32;
+    constexpr int BM = WM * TM * 32;
+    constexpr int TILE = BKT * (BO + BM);
+    constexpr int NCH = BM / 64;                 // 64-position chunks per input row
+    static_assert(NCH >= 1 && NCH <= 4 && 4 % NCH == 0, "BM in {64,128,256}");
+    constexpr int RSTEP = 4 / NCH;               // rows between one wave's consecutive input DMAs
+    constexpr int XI = BKT * NCH / 4;            // input DMAs per wave per step
+    constexpr int WF = BKT * BO;                 // floats in the weight slab
+    constexpr int WW = WeightDma<WF>::ww;         // floats per lane of a weight DMA
+    static_assert(WF % (256 * WW) == 0, "weight slab must split evenly over the 4 waves");
+    constexpr int WI = WF / (256 * WW);          // weight DMAs per wave per step
+    constexpr int PER = XI + WI;
+    static_assert(NST >= 2 && NST <= 4 && PER * (NST - 2) <= 63, "vmcnt range");
+    __shared__ __attribute__((aligned(16))) float smem[NST * TILE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: DMA bases / M0 need SGPRs
+    const int wo = wave / WM, wm = wave % WM;
+    const int phase = blockIdx.z / p.nsplit;
+    const int split = blockIdx.z - phase * p.nsplit;
+    const PhaseDev& ph = p.ph[phase];
+    const int hw_out = ph.out_h * ph.out_w;
+    const int M = p.n * hw_out;
+    const int m0 = blockIdx.x * BM;
+    if (m0 >= M) return;
+    const int o0 = blockIdx.y * BO;
+    const int cpk = p.cin / BKT;
+    const int ks_total = ph.ntaps * cpk;
+    const int ks_begin = (int)((int64_t)ks_total * split / p.nsplit);
+    const int ks_end = (int)((int64_t)ks_total * (split + 1) / p.nsplit);
+
+    // input DMAs: wave -> chunk cw (64 positions), rows r0 + RSTEP*j; lane -> one position
+    const int cw = wave % NCH, r0 = wave / NCH;
+    const int m = m0 + cw * 64 + lane;
+    const bool mvalid = m < M;
+    int nn = 0, a = 0, b = 0;
+    if (mvalid) {
+        nn = m / hw_out;
+        const int rem = m - nn * hw_out;
+        a = rem / ph.out_w;
+        b = rem - a * ph.out_w;
+    }
+    const int in_hw = p.in_h * p.in_w;
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * in_hw * 4), 0x00020000);
+    const int xvbase = nn * p.cin * in_hw * 4;
+    const int ay = a * ph.in_stride, bx = b * ph.in_stride;
+    // weight DMAs: this workgroup's sample (s != NULL) or the shared weights
+    const float* wk = ph.wk + (ph.wstride ? (int64_t)(m0 / hw_out) * ph.wstride : 0);
+
+    auto issue = [&](int ks, int slot) {
+        const int t = ks / cpk;
+        const int ci0 = (ks - t * cpk) * BKT;
+        const int iy = ay + ph.dy[t], ix = bx + ph.dx[t];
+        const bool ok = mvalid && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w;
+        const int voff = ok ? xvbase + (iy * p.in_w + ix) * 4 : 0x7ffffff0;
+        float* xs = smem + slot * TILE + BKT * BO;
 #pragma unroll
-    for (int j = 0; j < TM; ++j) {
-        const int mc = m0 + wm * TM * 32 + j * 32 + l32;
-        if (mc >= M) continue;
-        const int en = mc / hw_out;
-        const int erem = mc - en * hw_out;
-        const int ea = erem / ph.out_w;
-        const int eb = erem - ea * ph.out_w;
-        const int yy = ph.out_oy + ph.out_sy * ea;
-        const int xx = ph.out_ox + ph.out_sx * eb;
-        const int64_t pix = (int64_t)yy * p.y_w + xx;
-        const int64_t plane = (int64_t)p.y_h * p.y_w;
-        float nz = 0.f;
-        if (p.nsplit == 1 && p.mode == SMC_EPI_MODACT && p.noise) nz = p.noise[en * p.noise_nstride + pix] * nstr;
-#pragma unroll
-        for (int i = 0; i < TO; ++i) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int o = o0 + wo * TO * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-                if (o >= p.cout) continue;
-                const int64_t idx = ((int64_t)en * p.cout + o) * plane + pix;
-                const float v = acc[i][j][r];
-                if (p.nsplit > 1) {
-                    dst[idx] = v;
-                } else if (p.mode == SMC_EPI_MODACT) {
-                    if (p.u_save) p.u_save[idx] = v;
-                    const float dd = (p.d ? p.d[(int64_t)en * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
-                    float r = smc::epi_y(v, dd, nz, p.bias ? p.bias[o] : 0.f, p.act, p.alpha, p.gain, p.clamp);
-                    if (p.ext.residual) r = smc::epi_ext_apply(SMC_EPI_STORE, r, en, o, idx, yy, xx, p.cout, p.y_h, p.y_w,
-                                                                nullptr, nullptr, p.ext);
-                    dst[idx] = r;
-                } else {
-                    dst[idx] = smc::epi_ext_apply(p.mode, v, en, o, idx, yy, xx, p.cout, p.y_h, p.y_w, p.bias, p.u_save,
-                                                  p.ext);
-                }
-            }
+        for (int j = 0; j < XI; ++j) {
+            const int row = r0 + RSTEP * j;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                xrsrc, (__attribute__((address_space(3))) void*)(xs + row * BM + cw * 64), 4, voff,
+                (ci0 + row) * in_hw * 4, 0, 0);
         }
+        float* ws = smem + slot * TILE;
+        const float* wrow = wk + ((int64_t)t * p.cin + ci0) * p.cout + o0;
+#pragma unroll
+        for (int j = 0; j < WI; ++j) {
+            const int f0 = (wave + 4 * j) * 64 * WW;          // first float of this DMA in the slab
+            const int f = f0 + lane * WW;
+            const int row = f / BO, col = f - row * BO;
+            const void* src = (const void*)(wrow + (int64_t)row * p.cout + col);
+            auto* dst = (__attribute__((address_space(3))) void*)(ws + f0);
+            if constexpr (WW == 4) __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+            else __builtin_amdgcn_global_load_lds(src, dst, 4, 0, 0);
+        }
+    };
+
+    f32x16 acc[TO][TM];
+#pragma unroll
+    for (int i = 0; i < TO; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int kh = lane >> 5, l32 = lane & 31;
+    int issued = ks_begin;
+#pragma unroll
+    for (int q = 0; q < NST - 1; ++q) {
+        if (issued < ks_end) {
+            issue(issued, (issued - ks_begin) % NST);
+            ++issued;
+        }
+    }
+    for (int ks = ks_begin; ks < ks_end; ++ks) {
+        // this wave's DMAs for step ks are done once at most (issued - ks - 1) later steps remain in flight
+        const int ahead = issued - ks - 1;
+        if constexpr (NST == 2) {
+            wait_vmcnt<0>();
+        } else if constexpr (NST == 3) {
+            if (ahead >= 1) wait_vmcnt<PER>();
+            else wait_vmcnt<0>();
+        } else {
+            if (ahead >= 2) wait_vmcnt<2 * PER>();
+            else if (ahead == 1) wait_vmcnt<PER>();
+            else wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's DMAs for step ks have landed; slot ks-1 is free
+        asm volatile("" ::: "memory");
+        if (issued < ks_end) {
+            issue(issued, (issued - ks_begin) % NST);
+            ++issued;
+        }
+        const int slot = (ks - ks_begin) % NST;
+        const float* Ws = smem + slot * TILE;
+        const float* Xs = Ws + BKT * BO;
+        const float* wrow = Ws + kh * BO + wo * TO * 32 + l32;
+        const float* xrow = Xs + kh * BM + wm * TM * 32 + l32;
+#pragma unroll
+        for (int k0 = 0; k0 < BKT; k0 += 16) {
+            float af[8][TO], bf[8][TM];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+#pragma unroll
+                for (int i = 0; i < TO; ++i) af[q][i] = wrow[(k0 + 2 * q) * BO + i * 32];
+#pragma unroll
+                for (int j = 0; j < TM; ++j) bf[q][j] = xrow[(k0 + 2 * q) * BM + j * 32];
+            }
+            __builtin_amdgcn_sched_barrier(0);  // fragment reads first: the LDS latency is paid once per chunk
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+#pragma unroll
+                for (int i = 0; i < TO; ++i)
+#pragma unroll
+                    for (int j = 0; j < TM; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q][i], bf[q][j], acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragment reads of this slot done before the next barrier
+    }
+    gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32);
+}
+
+// Per-sample weights for the LDS-DMA kernel: out[n][row][o] = wk[row][o] * s[n][row % cin].
+__global__ __launch_bounds__(256) void wscale_kernel(const float* wk, const float* s, float* out, int rows, int cin,
+                                                     int cout, int n) {
+    const int64_t per = (int64_t)rows * cout / 4;
+    const int64_t total = per * n;
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < total; v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t nn = v / per;
+        const int64_t e = (v - nn * per) * 4;
+        const int row = (int)(e / cout);
+        float4 w = *reinterpret_cast<const float4*>(wk + e);
+        const float sc = s[nn * cin + row % cin];
+        w.x *= sc; w.y *= sc; w.z *= sc; w.w *= sc;
+        *reinterpret_cast<float4*>(out + nn * (int64_t)rows * cout + e) = w;
     }
 }
 
@@ -583,6 +778,49 @@ int plan_split(int n, int cin, int cout, const smc_conv_phase* ph, int nph, cons
     return s < 1 ? 1 : s;
 }
 
+// The LDS-DMA kernel covers full column tiles, 32-bit input offsets and (for a style-scaled input)
+// workgroups that never straddle two images.  `scaled_ok` reports the latter.
+bool lds_shape_ok(int n, int cin, int cout, int in_h, int in_w, const smc_conv_phase* ph, int nph, const Cfg& c,
+                  bool* scaled_ok) {
+    static const bool off = getenv("SMC_NO_LDS_DMA") != nullptr;  // A/B knob (tools/bench_gemm.py)
+    bool so = true;
+    for (int i = 0; i < nph; ++i) so = so && ((int64_t)ph[i].out_h * ph[i].out_w) % c.bm == 0;
+    if (scaled_ok) *scaled_ok = so;
+    return !off && cout % c.bo == 0 && cin % BK == 0 && (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31);
+}
+
+// floats of per-sample weights (n x sum_p taps_p * cin * cout), 64-float aligned
+int64_t wsample_floats(int n, int cin, int cout, const smc_conv_phase* ph, int nph) {
+    int64_t t = 0;
+    for (int i = 0; i < nph; ++i) t += (int64_t)ph[i].ntaps * cin * cout;
+    return ((t * n + 63) / 64) * 64;
+}
+
+// LDS ring depth per tile config (measured on MI355X, tools/bench_gemm.py, FFHQ-1024 shapes, batch 4):
+// two stages (32-41 KB of LDS -> 3-4 workgroups per CU) beat three or four on every layer: the
+// occupancy hides the DMA latency better than a deeper ring (total 12.6 vs 13.0 / 13.3 ms, register-
+// staged kernel 13.2 ms).  SMC_LDS_STAGES (wide 128x128 tile) / SMC_LDS_NARROW (32/64 x 256 tiles)
+// override the depth (2..4; 0 = register-staged kernel) for A/B runs.
+int lds_stages(int cfg) {
+    auto knob = [](const char* name) {
+        const char* f = getenv(name);
+        const int s = f ? atoi(f) : 2;
+        return s <= 0 ? 0 : (s < 2 ? 2 : (s > 4 ? 4 : s));
+    };
+    static const int wide = knob("SMC_LDS_STAGES");
+    static const int narrow = knob("SMC_LDS_NARROW");
+    return cfg == 0 ? wide : narrow;
+}
+
+// BK = 32 for the wide tile on the long-K 512-channel layers (SMC_LDS_BK32=0 disables)
+bool lds_bk32(int cfg, int cin) {
+    static const bool on = [] {
+        const char* f = getenv("SMC_LDS_BK32");
+        return !f || atoi(f) != 0;
+    }();
+    return on && cfg == 0 && cin % 32 == 0 && cin >= 512;
+}
+
 int validate(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h, int y_w,
              const smc_conv_phase* phases, int nphases) {
     SMC_CHECK(x && y && phases, "smc_conv_gemm_f32: null pointer");
@@ -623,13 +861,21 @@ SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, 
         s = plan_split_convt(n, cin, cout, (y_h - 1) / 2, (y_w - 1) / 2);
     else
         s = plan_split(n, cin, cout, phases, nphases, c);
-    return s > 1 ? (int64_t)s * n * cout * y_h * y_w * (int64_t)sizeof(float) : 0;
+    int64_t bytes = s > 1 ? (int64_t)s * n * cout * y_h * y_w * (int64_t)sizeof(float) : 0;
+    // the LDS-DMA kernel's per-sample weights when the input is style-scaled (the query does not know
+    // whether it will be: reserve whenever the shape qualifies)
+    bool scaled_ok = false;
+    // (input size 1x1: the query reserves for a superset of the launches that use the area)
+    if (lds_shape_ok(n, cin, cout, 1, 1, phases, nphases, c, &scaled_ok) && scaled_ok)
+        bytes = ((bytes + 255) / 256) * 256 + wsample_floats(n, cin, cout, phases, nphases) * (int64_t)sizeof(float);
+    return bytes;
 }
 
-SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h,
-                              int y_w, const smc_conv_phase* phases, int nphases, const float* s_in,
-                              const smc_conv_epilogue* epi, float* workspace, int64_t workspace_bytes,
-                              void* stream) {
+namespace {
+
+int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h, int y_w,
+                   const smc_conv_phase* phases, int nphases, const float* s_in, const smc_conv_epilogue* epi,
+                   float* workspace, int64_t workspace_bytes, void* stream, int tag) {
     int rc = validate(x, n, cin, in_h, in_w, y, cout, y_h, y_w, phases, nphases);
     if (rc != SMC_OK) return rc;
     Cfg c;
@@ -691,6 +937,49 @@ SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w
         return smc_modconv_epilogue_f32(workspace, nsplit, plane_elems, y, n, cout, y_h, y_w, &e, stream);
     }
     dim3 grid((unsigned)smc::ceil_div(max_m, c.bm), (unsigned)smc::ceil_div(cout, c.bo), (unsigned)(nphases * nsplit));
+    bool scaled_ok = false;
+    const int nst = lds_stages(cfg);
+    if (nst && lds_shape_ok(n, cin, cout, in_h, in_w, phases, nphases, c, &scaled_ok) && (!s_in || scaled_ok)) {
+        if (s_in) {
+            // per-sample weights W[t][i][o] * s[n][i], [phase][n][taps*cin][cout], after the split-K partials
+            const int64_t part = nsplit > 1 ? ((nsplit * plane_elems * (int64_t)sizeof(float) + 255) / 256) * 256 : 0;
+            const int64_t need = part + wsample_floats(n, cin, cout, phases, nphases) * (int64_t)sizeof(float);
+            SMC_CHECK(workspace && workspace_bytes >= need, "smc_conv_gemm_f32: workspace %lld < %lld bytes",
+                      (long long)workspace_bytes, (long long)need);
+            float* wsamp = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + part);
+            int64_t off = 0;
+            for (int i = 0; i < nphases; ++i) {
+                const int rows = phases[i].ntaps * cin;
+                const int64_t tot4 = (int64_t)rows * cout / 4 * n;
+                hipLaunchKernelGGL(wscale_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(tot4, 256), 4096)),
+                                   dim3(256), 0, st, phases[i].wk, s_in, wsamp + off, rows, cin, cout, n);
+                p.ph[i].wk = wsamp + off;
+                p.ph[i].wstride = (int64_t)rows * cout;
+                off += (int64_t)rows * cout * n;
+            }
+            rc = smc::check_launch("smc_conv_gemm_f32 (per-sample weights)");
+            if (rc != SMC_OK) return rc;
+        }
+        p.s = nullptr;
+#define SMC_LAUNCH_LDS(WO_, WM_, TO_, TM_)                                                                          \
+    do {                                                                                                          \
+        if (nst == 2 && tag) hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 2, 1>), grid, dim3(NT), 0, st, p); \
+        else if (nst == 2) hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 2>), grid, dim3(NT), 0, st, p); \
+        else if (nst == 3) hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 3>), grid, dim3(NT), 0, st, p); \
+        else hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 4>), grid, dim3(NT), 0, st, p);     \
+    } while (0)
+        if (cfg == 0 && lds_bk32(cfg, cin) && nst == 2 && tag)
+            hipLaunchKernelGGL((conv_gemm_lds_kernel<2, 2, 2, 2, 32, 2, 1>), grid, dim3(NT), 0, st, p);
+        else if (cfg == 0 && lds_bk32(cfg, cin) && nst == 2)
+            hipLaunchKernelGGL((conv_gemm_lds_kernel<2, 2, 2, 2, 32, 2>), grid, dim3(NT), 0, st, p);
+        else if (cfg == 0) SMC_LAUNCH_LDS(2, 2, 2, 2);
+        else if (cfg == 1) SMC_LAUNCH_LDS(1, 4, 2, 2);
+        else SMC_LAUNCH_LDS(1, 4, 1, 2);
+#undef SMC_LAUNCH_LDS
+        rc = smc::check_launch("smc_conv_gemm_f32 (LDS-DMA)");
+        if (rc != SMC_OK || nsplit == 1) return rc;
+        return smc_modconv_epilogue_f32(workspace, nsplit, plane_elems, y, n, cout, y_h, y_w, &e, stream);
+    }
     // BK=32 halves the barriers per FLOP; it pays on the long-K 512-channel layers, BK=16 (more
     // workgroups per CU: 32-40 KB LDS vs 64-80 KB) on the high-resolution ones (tools/bench_gemm.py).
     bool k32 = cin % 32 == 0 && cin >= 512;
@@ -699,7 +988,9 @@ SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w
     const bool buf = (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31) && !getenv("SMC_NO_BUFFER_LOADS");
 #define SMC_LAUNCH(WO_, WM_, TO_, TM_)                                                                       \
     do {                                                                                                   \
-        if (k32 && buf) hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 32, true>), grid, dim3(NT), 0, st, p);   \
+        if (k32 && buf && tag) hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 32, true, 1>), grid, dim3(NT), 0, st, p); \
+        else if (buf && tag) hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 16, true, 1>), grid, dim3(NT), 0, st, p); \
+        else if (k32 && buf) hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 32, true>), grid, dim3(NT), 0, st, p);   \
         else if (k32) hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 32, false>), grid, dim3(NT), 0, st, p);    \
         else if (buf) hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 16, true>), grid, dim3(NT), 0, st, p);     \
         else hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 16, false>), grid, dim3(NT), 0, st, p);             \
@@ -712,3 +1003,22 @@ SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w
     if (rc != SMC_OK || nsplit == 1) return rc;
     return smc_modconv_epilogue_f32(workspace, nsplit, plane_elems, y, n, cout, y_h, y_w, &e, stream);
 }
+
+}  // namespace
+
+SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h,
+                              int y_w, const smc_conv_phase* phases, int nphases, const float* s_in,
+                              const smc_conv_epilogue* epi, float* workspace, int64_t workspace_bytes,
+                              void* stream) {
+    return conv_gemm_impl(x, n, cin, in_h, in_w, y, cout, y_h, y_w, phases, nphases, s_in, epi, workspace,
+                          workspace_bytes, stream, 0);
+}
+
+namespace smc {
+int conv_gemm_aux(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h, int y_w,
+                  const smc_conv_phase* phases, int nphases, const float* s_in, const smc_conv_epilogue* epi,
+                  float* workspace, int64_t workspace_bytes, void* stream) {
+    return conv_gemm_impl(x, n, cin, in_h, in_w, y, cout, y_h, y_w, phases, nphases, s_in, epi, workspace,
+                          workspace_bytes, stream, 1);
+}
+}  // namespace smc

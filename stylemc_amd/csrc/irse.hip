@@ -327,7 +327,7 @@ SMC_API int smc_irse_forward_f32(const smc_irse_net* net, const float* img, int 
     if (saved) saved_floats(*net, n, saved, us.data(), &stem_z);
     auto conv = [&](const float* x, int cin, int ih, int iw, float* y, int cout, int yh, int yw,
                     const smc_conv_phase* ph, int nph, const smc_conv_epilogue& e) {
-        return smc_conv_gemm_f32(x, n, cin, ih, iw, y, cout, yh, yw, ph, nph, nullptr, &e, w.conv, w.conv_bytes,
+        return smc::conv_gemm_aux(x, n, cin, ih, iw, y, cout, yh, yw, ph, nph, nullptr, &e, w.conv, w.conv_bytes,
                                  stream);
     };
     const int H = net->in_h, W = net->in_w;
@@ -413,7 +413,7 @@ SMC_API int smc_irse_backward_f32(const smc_irse_net* net, const float* dfeat, i
     saved_floats(*net, n, const_cast<float*>(saved), us.data(), &stem_z);
     auto conv = [&](const float* x, int cin, int ih, int iw, float* y, int cout, int yh, int yw,
                     const smc_conv_phase* ph, int nph, const smc_conv_epilogue& e) {
-        return smc_conv_gemm_f32(x, n, cin, ih, iw, y, cout, yh, yw, ph, nph, nullptr, &e, w.conv, w.conv_bytes,
+        return smc::conv_gemm_aux(x, n, cin, ih, iw, y, cout, yh, yw, ph, nph, nullptr, &e, w.conv, w.conv_bytes,
                                  stream);
     };
     // d(flattened last output) = dfeat @ fc_w

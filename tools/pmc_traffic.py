@@ -1,4 +1,5 @@
-"""HBM traffic per launch of the conv_gemm_kernel family from two rocprofv3 --pmc passes.
+"""HBM traffic per launch of the synthesis modconv GEMM family (conv_gemm_lds_kernel / conv_gemm_kernel /
+convt_gemm_kernel, TAG 0) from two rocprofv3 --pmc passes.
 
     python tools/pmc_traffic.py FETCH.csv WRITE.csv > profiles/pmc_traffic.json
 
@@ -28,14 +29,18 @@ def per_dispatch(path, counter):
 def main():
     fetch, names = per_dispatch(sys.argv[1], "FETCH_SIZE")
     write, names_w = per_dispatch(sys.argv[2], "WRITE_SIZE")
-    fam_r = [v for d, v in fetch.items() if "conv_gemm_kernel" in names[d]]
-    fam_w = [v for d, v in write.items() if "conv_gemm_kernel" in names_w[d]]
+    def fam(n):
+        return ("conv_gemm" in n or "convt_gemm_kernel" in n) and ", 1>(" not in n
+
+    fam_r = [v for d, v in fetch.items() if fam(names[d])]
+    fam_w = [v for d, v in write.items() if fam(names_w[d])]
     rd = 2 * 1024 * sum(fam_r) / max(len(fam_r), 1)
     wr = 1024 * sum(fam_w) / max(len(fam_w), 1)
     out = {"conv_gemm_bytes_per_launch": round(rd + wr),
            "read_bytes_per_launch": round(rd), "write_bytes_per_launch": round(wr),
            "launches": [len(fam_r), len(fam_w)],
-           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes over bench.py --steps 2 --warmup 1; "
+           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes over bench.py --steps 2 --warmup 1 "
+                     "(+ its 2-step serialised roofline pass); "
                      "read = 2 x FETCH_SIZE KiB (gfx950 correction), write = WRITE_SIZE KiB"}
     print(json.dumps(out, indent=1))
 
