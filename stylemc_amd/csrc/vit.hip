@@ -223,10 +223,7 @@ int lin_nsplit(int M, int N, int K) {
 
 int64_t lin_tiles(int M, int N) { return smc::ceil_div(M, LBM) * smc::ceil_div(N, LBN); }
 
-int64_t lin_ws_floats(int M, int N, int K) {
-    const int s = lin_nsplit(M, N, K);
-    return s > 1 ? (int64_t)s * M * N : 0;
-}
+int64_t lin_ws_floats(int M, int N, int K);  // defined after the v2 kernel (same plan as lin_launch)
 
 int lin_validate(const float* a, int lda, const float* b, int ldb, const float* c, int ldc, int M, int N, int K) {
     SMC_CHECK(a && b && c, "smc_linear_f32: null pointer");
@@ -242,6 +239,146 @@ int lin_validate(const float* a, int lda, const float* b, int ldb, const float* 
     return SMC_OK;
 }
 
+// ------------------------------------------------------------------------------------------ GEMM v2
+// The default for K % 64 == 0, N % 64 == 0 (every ViT projection): a 32 x 64 output tile per 256-thread
+// workgroup, waves 2 x 2, each 16 rows x 32 columns = two v_mfma_f32_16x16x4_f32 accumulators (independent,
+// so they issue back to back despite the 40-cycle dependent latency).  Both operand tiles go global -> LDS
+// by global_load_lds_dwordx4 (no VGPR staging) into a 2-stage ring, BK = 64:
+//   A [32 rows][64 k]  row-major, float4 column c of row i stored at slot c ^ (i & 15): one ds_read_b128
+//                      gives a lane 4 consecutive k of its row, conflict-free over the 16 rows of a group;
+//   B [64 k][64 n]     row-major, float4 column c of row k stored at c ^ (((k >> 2) & 1) << 2): the two
+//                      k-rows a 32-lane ds_read_b32 group touches land 16 banks apart.
+// K order inside a 16-deep chunk is permuted consistently for A and B (lane group g = lane / 16 owns k
+// = 4g + s at MFMA step s), which is what lets A come from one 16-B read.  Tiles are laid out XCD-aware:
+// consecutive tiles share an N column block and go to the same XCD, so each weight tile is streamed into
+// one L2.
+constexpr int L2M = 32, L2N = 64, L2K = 64;
+
+__global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, int ntl) {
+    constexpr int ATILE = L2M * L2K, BTILE = L2K * L2N, STAGE = ATILE + BTILE;
+    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    // XCD-aware tile order (bijective for any grid size)
+    const int nb = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
+    const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int m_tile = lin % mt;
+    const int rest = lin / mt;
+    const int n_tile = rest % ntl;
+    const int split = rest / ntl;
+    const int m0 = m_tile * L2M, n0 = n_tile * L2N;
+    const int nks = p.K / L2K;
+    const int ks0 = (int)((int64_t)nks * split / p.nsplit);
+    const int ks1 = (int)((int64_t)nks * (split + 1) / p.nsplit);
+
+    auto issue = [&](int ks, int slot) {
+        float* As = smem + slot * STAGE;
+        float* Bs = As + ATILE;
+        const int k0 = ks * L2K;
+        // A: 512 float4 slots = 8 DMAs, 2 per wave; slot v -> row v/16, physical column v%16
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int base = (wave * 2 + j) * 256;           // float offset of this DMA in the tile
+            const int v = base / 4 + lane;
+            const int row = v >> 4, cphys = v & 15;
+            const int c = cphys ^ (row & 15);
+            const int grow = min(m0 + row, p.M - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(p.a + (int64_t)grow * p.lda + k0 + 4 * c),
+                                             (__attribute__((address_space(3))) void*)(As + base), 16, 0, 0);
+        }
+        // B: 1024 float4 slots = 16 DMAs, 4 per wave; slot v -> k-row v/16, physical column v%16
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int base = (wave * 4 + j) * 256;
+            const int v = base / 4 + lane;
+            const int krow = v >> 4, cphys = v & 15;
+            const int c = cphys ^ (((krow >> 2) & 1) << 2);
+            __builtin_amdgcn_global_load_lds((const void*)(p.b + (int64_t)(k0 + krow) * p.ldb + n0 + 4 * c),
+                                             (__attribute__((address_space(3))) void*)(Bs + base), 16, 0, 0);
+        }
+    };
+
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const int i = lane & 15, g = lane >> 4;  // A row / B column within the block, k group
+    const int arow = wm * 16 + i;
+    if (ks0 < ks1) issue(ks0, 0);
+    for (int ks = ks0; ks < ks1; ++ks) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (ks + 1 < ks1) issue(ks + 1, (ks + 1 - ks0) & 1);
+        const float* As = smem + ((ks - ks0) & 1) * STAGE;
+        const float* Bs = As + ATILE;
+#pragma unroll
+        for (int kc = 0; kc < L2K; kc += 16) {
+            // A: row arow, k = kc + 4g .. +3 -> logical float4 column (kc/4 + g)
+            const int ca = (kc / 4 + g) ^ (arow & 15);
+            const f32x4 av = *reinterpret_cast<const f32x4*>(As + arow * L2K + 4 * ca);
+            float bv[2][4];
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const int krow = kc + 4 * g + s2;
+                const int sw = ((krow >> 2) & 1) << 2;
+#pragma unroll
+                for (int blk = 0; blk < 2; ++blk) {
+                    const int n = wn * 32 + blk * 16 + i;
+                    bv[blk][s2] = Bs[krow * L2N + 4 * ((n >> 2) ^ sw) + (n & 3)];
+                }
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+                for (int blk = 0; blk < 2; ++blk)
+                    acc[blk] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], bv[blk][s2], acc[blk], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    // epilogue: block blk, register rr -> row 4g + rr, column i
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+        const int n = n0 + wn * 32 + blk * 16 + i;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int m = m0 + wm * 16 + 4 * g + rr;
+            if (m >= p.M) continue;
+            if (p.nsplit > 1)
+                p.ws[((int64_t)split * p.M + m) * p.N + n] = acc[blk][rr];
+            else
+                p.c[(int64_t)m * p.ldc + n] = lin_epi(acc[blk][rr], m, n, p.e);
+        }
+    }
+}
+
+bool lin_v2_ok(int N, int K, int lda, int ldb) {
+    static const bool off = getenv("SMC_LIN_V1") != nullptr;  // A/B knob (tools/bench_linear.py)
+    return !off && K % L2K == 0 && N % L2N == 0 && lda % 4 == 0 && ldb % 4 == 0;
+}
+
+int lin_nsplit2(int M, int N, int K) {
+    const int64_t tiles = smc::ceil_div(M, L2M) * (N / L2N);
+    const int nks = K / L2K;
+    const int64_t cus = smc::device_cu_count();
+    int best = 1;
+    int64_t best_cost = -1;
+    for (int s = 1; s <= 16 && s <= nks; ++s) {
+        const int64_t cost = smc::ceil_div(tiles * s, cus) * (smc::ceil_div(nks, s) + 2) + (s > 1 ? 1 : 0);
+        if (best_cost < 0 || cost < best_cost) {
+            best_cost = cost;
+            best = s;
+        }
+    }
+    return best;
+}
+
+int64_t lin_ws_floats(int M, int N, int K) {
+    // v2 needs lda/ldb % 4 == 0, which every caller guarantees (lin_validate rejects the rest)
+    const int s = lin_v2_ok(N, K, 4, 4) ? lin_nsplit2(M, N, K) : lin_nsplit(M, N, K);
+    return s > 1 ? (int64_t)s * M * N : 0;
+}
+
 int lin_launch(const float* a, int lda, const float* b, int ldb, float* c, int ldc, int M, int N, int K,
                const smc_linear_epilogue* epi, float* ws, int64_t ws_bytes, hipStream_t st, int* counters = nullptr) {
     int rc = lin_validate(a, lda, b, ldb, c, ldc, M, N, K);
@@ -249,16 +386,22 @@ int lin_launch(const float* a, int lda, const float* b, int ldb, float* c, int l
     LinParams p{};
     p.a = a; p.lda = lda; p.b = b; p.ldb = ldb; p.c = c; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
     if (epi) p.e = *epi;
-    p.nsplit = lin_nsplit(M, N, K);
+    const bool v2 = lin_v2_ok(N, K, lda, ldb);
+    p.nsplit = v2 ? lin_nsplit2(M, N, K) : lin_nsplit(M, N, K);
     if (p.nsplit > 1) {
         const int64_t need = (int64_t)p.nsplit * M * N * (int64_t)sizeof(float);
         SMC_CHECK(ws && ws_bytes >= need, "smc_linear_f32: workspace %lld < %lld bytes", (long long)ws_bytes,
                   (long long)need);
         p.ws = ws;
-        p.counters = counters;
+        p.counters = v2 ? nullptr : counters;
     }
-    dim3 grid((unsigned)smc::ceil_div(M, LBM), (unsigned)smc::ceil_div(N, LBN), (unsigned)p.nsplit);
-    hipLaunchKernelGGL(lin_gemm_kernel, grid, dim3(LNT), 0, st, p);
+    if (v2) {
+        const int mt = (int)smc::ceil_div(M, L2M), ntl = N / L2N;
+        hipLaunchKernelGGL(lin_gemm2_kernel, dim3((unsigned)(mt * ntl * p.nsplit)), dim3(256), 0, st, p, mt, ntl);
+    } else {
+        dim3 grid((unsigned)smc::ceil_div(M, LBM), (unsigned)smc::ceil_div(N, LBN), (unsigned)p.nsplit);
+        hipLaunchKernelGGL(lin_gemm_kernel, grid, dim3(LNT), 0, st, p);
+    }
     rc = smc::check_launch("smc_linear_f32");
     if (rc != SMC_OK || p.nsplit == 1 || p.counters) return rc;
     const int64_t nv = (int64_t)M * (N / 4);
