@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timer", action="store_true", help="skip the roofline pass")
     p.add_argument("--roofline-steps", type=int, default=2, help="serialised steps timed per launch for the roofline")
+    p.add_argument("--no-batch-losses", action="store_true",
+                   help="run the original image's loss-network forwards separately (on the side stream)")
     return p.parse_args()
 
 
@@ -132,7 +134,8 @@ def main():
                              "a photo of a face of a masculine man", impl=args.clip_impl)
     finder = DirectionFinder(G, styles, clip, IDLoss("a", device=dev, weights=None, impl=args.id_impl), resolution=args.resolution,
                              batch_size=args.batch, global_batch=args.batch * world.world_size, seed=0, world=world,
-                             init_delta=initial_delta(0, 0.01), n_epochs=1000)
+                             init_delta=initial_delta(0, 0.01), n_epochs=1000,
+                             batch_losses=not args.no_batch_losses)
     for _ in range(args.warmup):
         finder.step()
     torch.cuda.synchronize()
@@ -198,7 +201,8 @@ def main():
                                f"IR-SE50 fwd/bwd ({'HIP' if args.id_impl == 'hip' else 'PyTorch-ROCm'}), SGD",
                    "resolution": args.resolution, "batch_per_gpu": args.batch,
                    "global_batch": args.batch * world.world_size, "seeds_per_sec": round(seeds / dt, 3),
-                   "parallelism": f"dp{world.world_size}", "clip_type": args.clip_type, "clip_impl": args.clip_impl, "id_impl": args.id_impl, "landmarks_loss_coef": 0,
+                   "parallelism": f"dp{world.world_size}", "clip_type": args.clip_type, "clip_impl": args.clip_impl, "id_impl": args.id_impl,
+                   "batched_loss_pairs": finder.batch_losses, "landmarks_loss_coef": 0,
                    "direction_finite": finite},
         "roofline": roofline,
         "cpu_baseline": None,

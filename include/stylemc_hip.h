@@ -244,8 +244,10 @@ int64_t smc_vit_workspace_bytes(const smc_vit_config* cfg, int batch);
 /* image [batch][in_ch][grid*patch][grid*patch] -> out [batch][out_dim]; saved may be NULL (no backward). */
 int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, const float* image, int batch, float* out,
                         float* saved, float* workspace, int64_t workspace_bytes, void* stream);
-/* dimage = d out / d image applied to dout [batch][out_dim], from the forward's saved activations. */
-int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed, const float* dout, int batch,
+/* dimage = d out / d image applied to dout, from the forward's saved activations (laid out for `batch`
+ * images); only the leading batch_run <= batch images are differentiated: dout [batch_run][out_dim],
+ * dimage [batch_run][in_ch][..][..] (the original-image half of a batched pair needs no gradient). */
+int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed, const float* dout, int batch, int batch_run,
                          const float* saved, float* dimage, float* workspace, int64_t workspace_bytes,
                          void* stream);
 
@@ -301,8 +303,10 @@ int64_t smc_irse_workspace_bytes(const smc_irse_net* net, int n);
 /* img [n][img_ch][in_h][in_w] -> feat [n][feat] (before the l2 normalisation); saved may be NULL. */
 int smc_irse_forward_f32(const smc_irse_net* net, const float* img, int n, float* feat, float* saved,
                          float* workspace, int64_t workspace_bytes, void* stream);
-int smc_irse_backward_f32(const smc_irse_net* net, const float* dfeat, int n, const float* saved, float* dimg,
-                          float* workspace, int64_t workspace_bytes, void* stream);
+/* input gradient of the leading n <= n_saved faces of a forward that ran (and saved) n_saved faces:
+ * dfeat [n][feat] -> dimg [n][img_ch][in_h][in_w]. */
+int smc_irse_backward_f32(const smc_irse_net* net, const float* dfeat, int n_saved, int n, const float* saved,
+                          float* dimg, float* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -77,11 +77,11 @@ _SIGS = {
     "smc_vit_saved_floats": (c_int64, [P, c_int]),
     "smc_vit_workspace_bytes": (c_int64, [P, c_int]),
     "smc_vit_forward_f32": (c_int, [P, P, P, c_int, P, P, P, c_int64, P]),
-    "smc_vit_backward_f32": (c_int, [P, P, P, c_int, P, P, P, c_int64, P]),
+    "smc_vit_backward_f32": (c_int, [P, P, P, c_int, c_int, P, P, P, c_int64, P]),
     "smc_irse_saved_floats": (c_int64, [P, c_int]),
     "smc_irse_workspace_bytes": (c_int64, [P, c_int]),
     "smc_irse_forward_f32": (c_int, [P, P, c_int, P, P, P, c_int64, P]),
-    "smc_irse_backward_f32": (c_int, [P, P, c_int, P, P, P, c_int64, P]),
+    "smc_irse_backward_f32": (c_int, [P, P, c_int, c_int, P, P, P, c_int64, P]),
 }
 
 _lib = None

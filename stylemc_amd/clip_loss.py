@@ -42,6 +42,16 @@ class CLIPLoss(nn.Module):
         f = f / f.norm(dim=1, keepdim=True)
         return 1 - F.cosine_similarity(f, self.text_features)
 
+    def per_sample_pair(self, tgt_image, src_image):
+        """per_sample(src, tgt) with both images in ONE tower batch [tgt; src]: the backward runs for the
+        tgt half only (E(src) carries no gradient in the reference)."""
+        n = tgt_image.shape[0]
+        x = torch.cat([tgt_image, src_image.detach()])
+        e = self.visual(x, n_grad=n) if getattr(self.visual, "supports_partial_grad", False) else self.visual(x)
+        f = e[:n] - e[n:].detach()
+        f = f / f.norm(dim=1, keepdim=True)
+        return 1 - F.cosine_similarity(f, self.text_features)
+
     def per_sample(self, src_image, tgt_image):
         return self.per_sample_with(self.encode_src(src_image), tgt_image)
 

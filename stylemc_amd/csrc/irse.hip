@@ -399,18 +399,20 @@ SMC_API int smc_irse_forward_f32(const smc_irse_net* net, const float* img, int 
                           w.conv_bytes, stream);
 }
 
-SMC_API int smc_irse_backward_f32(const smc_irse_net* net, const float* dfeat, int n, const float* saved, float* dimg,
-                                  float* workspace, int64_t workspace_bytes, void* stream) {
-    SMC_TRY(net_validate(net, n));
+SMC_API int smc_irse_backward_f32(const smc_irse_net* net, const float* dfeat, int n_saved, int n, const float* saved,
+                                  float* dimg, float* workspace, int64_t workspace_bytes, void* stream) {
+    SMC_TRY(net_validate(net, n_saved));
     SMC_CHECK(dfeat && saved && dimg && workspace, "smc_irse_backward_f32: null pointer");
+    SMC_CHECK(n >= 1 && n <= n_saved, "smc_irse_backward_f32: n %d not in [1, %d]", n, n_saved);
     SMC_CHECK(workspace_bytes >= ws_floats(*net, n, nullptr, nullptr) * (int64_t)sizeof(float),
               "smc_irse_backward_f32: workspace too small");
     hipStream_t st = smc::as_stream(stream);
     Ws w;
     ws_floats(*net, n, workspace, &w);
+    // saved activations laid out for n_saved faces; the leading n are differentiated ([n_saved][C][H][W] prefixes)
     std::vector<UnitS> us(net->n_units);
     float* stem_z = nullptr;
-    saved_floats(*net, n, const_cast<float*>(saved), us.data(), &stem_z);
+    saved_floats(*net, n_saved, const_cast<float*>(saved), us.data(), &stem_z);
     auto conv = [&](const float* x, int cin, int ih, int iw, float* y, int cout, int yh, int yw,
                     const smc_conv_phase* ph, int nph, const smc_conv_epilogue& e) {
         return smc::conv_gemm_aux(x, n, cin, ih, iw, y, cout, yh, yw, ph, nph, nullptr, &e, w.conv, w.conv_bytes,

@@ -1150,12 +1150,16 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
 }
 
 SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed, const float* dout, int batch,
-                                 const float* saved, float* dimage, float* workspace, int64_t workspace_bytes,
-                                 void* stream) {
+                                 int batch_run, const float* saved, float* dimage, float* workspace,
+                                 int64_t workspace_bytes, void* stream) {
     SMC_TRY(vit_validate(cfg, batch));
     SMC_CHECK(packed && dout && saved && dimage && workspace, "smc_vit_backward_f32: null pointer");
+    SMC_CHECK(batch_run >= 1 && batch_run <= batch, "smc_vit_backward_f32: batch_run %d not in [1, %d]", batch_run,
+              batch);
     const VitDims d = dims(*cfg);
-    const int B = batch, M = B * d.L, D = d.D, Mt = B * d.G * d.G;
+    // the saved activations are laid out for `batch` images; the leading `batch_run` of them are
+    // differentiated (every per-image block of the layout is a prefix of its [batch * ...] tensor)
+    const int B = batch_run, M = B * d.L, D = d.D, Mt = B * d.G * d.G;
     SMC_CHECK(workspace_bytes >= ws_layout(d, B, nullptr, nullptr) * (int64_t)sizeof(float),
               "smc_vit_backward_f32: workspace too small");
     hipStream_t st = smc::as_stream(stream);
@@ -1164,7 +1168,7 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
     VitWs ws;
     ws_layout(d, B, workspace, &ws);
     VitS sv;
-    saved_layout(d, B, const_cast<float*>(saved), &sv);
+    saved_layout(d, batch, const_cast<float*>(saved), &sv);
     int64_t cursor = 0;
     auto lin = [&](const float* a, int lda, const float* bw, int ldb, float* c, int ldc, int MM, int N, int K,
                    const smc_linear_epilogue& e) {
@@ -1195,7 +1199,7 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
     float* dx = ws.dx;  // gradient w.r.t. the current layer's output stream (updated in place)
     for (int l = d.NL - 1; l >= 0; --l) {
         const LayerW lw = layer_w(d, w, l);
-        const LayerS ls = saved_layer(d, B, sv, l);
+        const LayerS ls = saved_layer(d, batch, sv, l);
         // MLP block
         smc_linear_epilogue e = epi_none();
         e.dact_pre = ls.G;

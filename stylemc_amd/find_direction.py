@@ -64,10 +64,13 @@ class DirectionFinder:
     def __init__(self, G, styles_array, clip_losses, id_loss, resolution=1024, batch_size=4, learning_rate=1.5,
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
-                 overlap=True):
+                 overlap=True, batch_losses=True):
         self.G = G
         self.synth_fn = synth_fn or utils.generate_image_rows   # (G, until_k, styles, shapes, noise, delta=)
         self.overlap = overlap                                  # original-image branch on a second stream
+        # edited + original image through each loss network as ONE batch (backward for the edited half)
+        self.batch_losses = batch_losses and hasattr(id_loss, "per_sample_pair") and all(
+            hasattr(cl, "per_sample_pair") for cl, _ in clip_losses)
         self.device = styles_array.device
         self.styles_array = styles_array
         self.clip_losses = clip_losses            # [(CLIPLoss, weight)], 'double' -> [(B/32, 1), (B/16, .5)]
@@ -110,6 +113,29 @@ class DirectionFinder:
             src_embs = [cl.encode_src(src) for cl, _ in self.clip_losses]
         return y_feats, src_embs
 
+    def _pair_terms(self, styles, d):
+        """Batched-loss form: the original image's synthesis (no gradient) runs on the second stream
+        beside the edited one; then each loss network sees [edited; original] as one batch."""
+        side = self._side_stream()
+        if side is not None:
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side), torch.no_grad():
+                orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
+            img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+            main.wait_stream(side)
+            orig.record_stream(main)
+        else:
+            img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+            with torch.no_grad():
+                orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
+        id_terms = self.id_loss.per_sample_pair(img, orig)
+        tgt = unprocess(img, self.mean, self.std)
+        with torch.no_grad():
+            src = unprocess(orig, self.mean, self.std)
+        clip_terms = sum(w * cl.per_sample_pair(tgt, src) for cl, w in self.clip_losses)
+        return id_terms, clip_terms
+
     def _local_terms(self, styles, denom):
         """Sum-form loss of this rank's shard: every per-sample term / global batch size.
 
@@ -118,6 +144,9 @@ class DirectionFinder:
         """
         T = S_TRAINABLE_SPACE_CHANNELS
         d = self.delta.detach().clone().requires_grad_(True)
+        if self.batch_losses:
+            id_terms, clip_terms = self._pair_terms(styles, d)
+            return self._finish(styles, d, id_terms, clip_terms, denom)
         side = self._side_stream()
         if side is not None:
             main = torch.cuda.current_stream()
@@ -134,6 +163,10 @@ class DirectionFinder:
         id_terms = self.id_loss.per_sample_with(img, y_feats)
         tgt = unprocess(img, self.mean, self.std)
         clip_terms = sum(w * cl.per_sample_with(e, tgt) for (cl, w), e in zip(self.clip_losses, src_embs))
+        return self._finish(styles, d, id_terms, clip_terms, denom)
+
+    def _finish(self, styles, d, id_terms, clip_terms, denom):
+        T = S_TRAINABLE_SPACE_CHANNELS
         sT = styles[:, T]
         l2_sum = ((sT + d) - sT).square().sum()
         id_part = self.coef["id"] * id_terms.sum() / denom

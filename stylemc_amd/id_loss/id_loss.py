@@ -32,12 +32,27 @@ class IDLoss(nn.Module):
         self.facenet = facenet.eval()
         self.opts = opts
 
-    def extract_feats(self, x):
+    @staticmethod
+    def face_crop(x):
+        """id_loss.py:20-23: pool to 256, crop [35:223, 32:220], pool to 112."""
         if x.shape[2] != 256:
             x = F.adaptive_avg_pool2d(x, (256, 256))
         x = x[:, :, 35:223, 32:220]
-        x = F.adaptive_avg_pool2d(x, (112, 112))
-        return self.facenet(x)
+        return F.adaptive_avg_pool2d(x, (112, 112))
+
+    def extract_feats(self, x):
+        return self.facenet(self.face_crop(x))
+
+    def per_sample_pair(self, y_hat, y):
+        """per_sample(y_hat, y) with both faces in ONE backbone batch [y_hat; y]: the backward runs for
+        the y_hat half only (y's features are detached in the reference, id_loss.py:32)."""
+        n = y_hat.shape[0]
+        a = self.face_crop(y_hat)
+        with torch.no_grad():
+            b = self.face_crop(y)
+        x = torch.cat([a, b])
+        f = self.facenet(x, n_grad=n) if getattr(self.facenet, "supports_partial_grad", False) else self.facenet(x)
+        return 1 - (f[:n] * f[n:].detach()).sum(dim=1)
 
     @torch.no_grad()
     def target_feats(self, y):

@@ -189,8 +189,10 @@ class _Packed:
 
 
 class _IrseFn(torch.autograd.Function):
+    """Backbone forward (features before the l2 norm) / input gradient of the leading n_grad faces."""
+
     @staticmethod
-    def forward(ctx, x, mod):
+    def forward(ctx, x, mod, n_grad=None):
         if not x.is_cuda:
             raise RuntimeError("HipIRSE50 runs on the GPU only (got a CPU tensor)")
         x = x.to(torch.float32).contiguous()
@@ -209,22 +211,25 @@ class _IrseFn(torch.autograd.Function):
         _hip.call("smc_irse_forward_f32", net, x.data_ptr(), n, feat.data_ptr(), _hip.ptr(saved), ws.data_ptr(), wsb,
                   _hip.stream())
         ctx.mod, ctx.saved_buf, ctx.shape = mod, saved, x.shape
+        ctx.n_grad = n if n_grad is None else int(n_grad)
+        if not 1 <= ctx.n_grad <= n:
+            raise ValueError(f"n_grad {n_grad} not in [1, {n}]")
         return feat
 
     @staticmethod
     def backward(ctx, gfeat):
         pk = ctx.mod.packed_net()
         net = ctypes.byref(pk.net)
-        gfeat = gfeat.to(torch.float32).contiguous()
-        n = ctx.shape[0]
+        n, nr = ctx.shape[0], ctx.n_grad
+        gfeat = gfeat[:nr].to(torch.float32).contiguous()
         lib = _hip.load()
-        dx = torch.empty(ctx.shape, device=gfeat.device, dtype=torch.float32)
-        wsb = lib.smc_irse_workspace_bytes(net, n)
+        dx = (torch.empty if nr == n else torch.zeros)(ctx.shape, device=gfeat.device, dtype=torch.float32)
+        wsb = lib.smc_irse_workspace_bytes(net, nr)
         ws = torch.empty(wsb // 4, device=gfeat.device, dtype=torch.float32)
-        _hip.call("smc_irse_backward_f32", net, gfeat.data_ptr(), n, ctx.saved_buf.data_ptr(), dx.data_ptr(),
+        _hip.call("smc_irse_backward_f32", net, gfeat.data_ptr(), n, nr, ctx.saved_buf.data_ptr(), dx.data_ptr(),
                   ws.data_ptr(), wsb, _hip.stream())
         ctx.saved_buf = None
-        return dx, None
+        return dx, None, None
 
 
 class HipIRSE50(nn.Module):
@@ -255,8 +260,11 @@ class HipIRSE50(nn.Module):
             self._packed = _Packed(self.body_net.eval(), dev, self.input_size)
         return self._packed
 
-    def forward(self, x):
-        f = _IrseFn.apply(x, self)
+    supports_partial_grad = True
+
+    def forward(self, x, n_grad=None):
+        """n_grad: back-propagate only the leading n_grad faces (the rest get a zero gradient)."""
+        f = _IrseFn.apply(x, self, n_grad)
         return f / torch.norm(f, 2, 1, True)   # model_irse.py:48 l2_norm
 
 

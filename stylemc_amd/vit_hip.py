@@ -58,8 +58,12 @@ def pack_weights(state_dict, layers):
 
 
 class _VitFn(torch.autograd.Function):
+    """Whole-tower forward / data gradient.  n_grad < batch: only the leading n_grad images are
+    differentiated (the rest of the batch -- the original images of a batched pair -- get a zero gradient
+    without being back-propagated)."""
+
     @staticmethod
-    def forward(ctx, image, mod):
+    def forward(ctx, image, mod, n_grad):
         if not image.is_cuda:
             raise RuntimeError("HipVisionTransformer runs on the GPU only (got a CPU tensor)")
         image = image.to(torch.float32).contiguous()
@@ -78,22 +82,25 @@ class _VitFn(torch.autograd.Function):
         _hip.call("smc_vit_forward_f32", cfg, mod.packed.data_ptr(), image.data_ptr(), B, out.data_ptr(),
                   _hip.ptr(saved), ws.data_ptr(), ws_bytes, _hip.stream())
         ctx.mod, ctx.saved_buf, ctx.shape = mod, saved, image.shape
+        ctx.n_grad = B if n_grad is None else int(n_grad)
+        if not 1 <= ctx.n_grad <= B:
+            raise ValueError(f"n_grad {n_grad} not in [1, {B}]")
         return out
 
     @staticmethod
     def backward(ctx, gout):
         mod, saved = ctx.mod, ctx.saved_buf
-        gout = gout.to(torch.float32).contiguous()
-        B = ctx.shape[0]
+        B, nr = ctx.shape[0], ctx.n_grad
+        gout = gout[:nr].to(torch.float32).contiguous()
         lib = _hip.load()
         cfg = ctypes_ref(mod.cfg)
-        dimage = torch.empty(ctx.shape, device=gout.device, dtype=torch.float32)
+        dimage = (torch.empty if nr == B else torch.zeros)(ctx.shape, device=gout.device, dtype=torch.float32)
         ws_bytes = lib.smc_vit_workspace_bytes(cfg, B)
         ws = torch.empty(ws_bytes // 4, device=gout.device, dtype=torch.float32)
-        _hip.call("smc_vit_backward_f32", cfg, mod.packed.data_ptr(), gout.data_ptr(), B, saved.data_ptr(),
+        _hip.call("smc_vit_backward_f32", cfg, mod.packed.data_ptr(), gout.data_ptr(), B, nr, saved.data_ptr(),
                   dimage.data_ptr(), ws.data_ptr(), ws_bytes, _hip.stream())
         ctx.saved_buf = None
-        return dimage, None
+        return dimage, None, None
 
 
 def ctypes_ref(cfg):
@@ -137,10 +144,13 @@ class HipVisionTransformer(nn.Module):
     def flops_per_image(self):
         return self.tower.flops_per_image()
 
-    def forward(self, image):
+    supports_partial_grad = True
+
+    def forward(self, image, n_grad=None):
+        """n_grad: differentiate only the leading n_grad images of the batch (see _VitFn)."""
         if self.packed.numel() == 0:
             self.refresh()
-        return _VitFn.apply(image, self)
+        return _VitFn.apply(image, self, n_grad)
 
 
 def build_visual(name="ViT-B/32", state_dict=None, seed=0, device="cuda"):

@@ -63,6 +63,11 @@ class OracleID(torch.nn.Module):
     def per_sample(self, y_hat, y):
         return self.per_sample_with(y_hat, self.target_feats(y))
 
+    def per_sample_pair(self, y_hat, y):
+        n = y_hat.shape[0]
+        f = self.inner.extract_feats(torch.cat([y_hat, y.detach()]))
+        return 1 - (f[:n] * f[n:].detach()).sum(1)
+
 
 class OracleCLIP(torch.nn.Module):
     def __init__(self, visual, text):
@@ -79,6 +84,13 @@ class OracleCLIP(torch.nn.Module):
 
     def per_sample(self, src, tgt):
         return self.per_sample_with(self.encode_src(src), tgt)
+
+    def per_sample_pair(self, tgt, src):
+        n = tgt.shape[0]
+        e = self.inner.visual(torch.cat([tgt, src.detach()]))
+        f = e[:n] - e[n:].detach()
+        f = f / f.norm(dim=1, keepdim=True)
+        return 1 - torch.nn.functional.cosine_similarity(f, self.inner.text_features)
 
 
 class TinyFace(torch.nn.Module):

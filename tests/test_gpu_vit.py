@@ -235,3 +235,38 @@ def test_vit_no_grad_matches_grad_path_and_torch_impl():
     tv = clip_model.build_visual("ViT-B/32", seed=4, device=DEV)
     with torch.no_grad():
         close(y0, tv(xg), 1e-4, "hip vs torch tower")
+
+
+@pytest.mark.parametrize("B,n", [(8, 4), (2, 1), (5, 3)])
+def test_vit_partial_backward(B, n):
+    """n_grad < B (batched [edited; original] pair): the gradient of the leading n images equals the
+    full backward with a zero cotangent for the rest, and the rest get exactly zero."""
+    hip, _, x, cot = _vit_pair("ViT-B/32", B)
+    cot[n:] = 0
+    xg = x.to(DEV).requires_grad_(True)
+    (dfull,) = torch.autograd.grad(hip(xg), xg, cot.to(DEV))
+    xp = x.to(DEV).requires_grad_(True)
+    yp = hip(xp, n_grad=n)
+    (dpart,) = torch.autograd.grad(yp, xp, cot.to(DEV))
+    assert torch.count_nonzero(dpart[n:]) == 0
+    close(dpart[:n], dfull[:n], 1e-4, f"B={B} n_grad={n} image gradient")
+
+
+def test_clip_pair_loss_equals_separate_encodes():
+    """CLIPLoss.per_sample_pair (one tower batch) == per_sample (two encodes), values and gradient."""
+    from stylemc_amd import vit_hip
+    from stylemc_amd.clip_loss import CLIPLoss
+    hip = vit_hip.build_visual("ViT-B/32", seed=4, device=DEV)
+    g = torch.Generator().manual_seed(1)
+    text = torch.nn.functional.normalize(torch.randn(1, 512, generator=g), dim=1).to(DEV)
+    cl = CLIPLoss(device=DEV, visual=hip, text_features=text)
+    src = torch.randn(3, 3, 224, 224, generator=g).to(DEV)
+    tgt = (src + 0.1 * torch.randn(src.shape, generator=g).to(DEV))
+    t1 = tgt.clone().requires_grad_(True)
+    l1 = cl.per_sample(src, t1)
+    (g1,) = torch.autograd.grad(l1.sum(), t1)
+    t2 = tgt.clone().requires_grad_(True)
+    l2 = cl.per_sample_pair(t2, src)
+    (g2,) = torch.autograd.grad(l2.sum(), t2)
+    close(l2, l1, 1e-5, "pair vs separate loss")
+    close(g2, g1, 1e-4, "pair vs separate gradient")

@@ -48,7 +48,7 @@ def main():
         mod = irse_hip.HipIRSE50()
         mod._packed = pk
         xg = x.cuda().requires_grad_(True)
-        yg = irse_hip._IrseFn.apply(xg, mod)
+        yg = irse_hip._IrseFn.apply(xg, mod, None)
         (dxg,) = torch.autograd.grad(yg, xg, cot.cuda())
         ey = ((yg.cpu().double() - yr).abs().max() / yr.abs().max()).item()
         d = (dxg.cpu().double() - dxr).abs()
