@@ -201,16 +201,35 @@ __global__ __launch_bounds__(256) void blur_act_fast(const float* t, int nsplit,
     load_taps<FH, FW>(f, flip, fgain, tp);
     const int iy0 = oy0 - pady0, ix0 = ox0 - padx0;
     const float* tpl = t + nc * (int64_t)t_h * t_w;
-    for (int i = tid; i < ROWS * COLS; i += 256) {
+    // Haloed tile load with a fixed, unrolled trip count: every load of the thread is in flight before
+    // the first LDS store (a data-dependent loop serialises one HBM latency per element).  Out-of-range
+    // elements load the plane's first float (always valid) and are zeroed by select.
+    constexpr int NL = (ROWS * COLS + 255) / 256;
+    float v[NL];
+    int off[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        const int i = tid + 256 * l;
         const int r = i / COLS, cc = i - r * COLS;
         const int iy = iy0 + r, ix = ix0 + cc;
-        float v = 0.f;
-        if (iy >= 0 && iy < t_h && ix >= 0 && ix < t_w) {
-            const int64_t off = (int64_t)iy * t_w + ix;
-            v = tpl[off];
-            for (int s = 1; s < nsplit; ++s) v += tpl[s * split_stride + off];
+        const bool ok = i < ROWS * COLS && iy >= 0 && iy < t_h && ix >= 0 && ix < t_w;
+        off[l] = ok ? iy * t_w + ix : -1;
+        const float a = tpl[ok ? off[l] : 0];
+        v[l] = ok ? a : 0.f;
+    }
+    for (int s = 1; s < nsplit; ++s) {
+        const float* sp = tpl + s * split_stride;
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            const float a = sp[off[l] >= 0 ? off[l] : 0];
+            v[l] += off[l] >= 0 ? a : 0.f;
         }
-        tile[r * STRIDE + cc] = v;
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        const int i = tid + 256 * l;
+        const int r = i / COLS, cc = i - r * COLS;
+        if (i < ROWS * COLS) tile[r * STRIDE + cc] = v[l];
     }
     __syncthreads();
     float out[4][2];
@@ -219,23 +238,45 @@ __global__ __launch_bounds__(256) void blur_act_fast(const float* t, int nsplit,
     const float dv = e.d ? e.d[nc] : 1.f;
     const float bv = e.bias ? e.bias[o] : 0.f;
     const int64_t plane = nc * (int64_t)y_h * y_w;
+    const int ox = ox0 + 2 * tx;
+    if (ox >= y_w) return;
+    // y_w even (all synthesis resolutions) and ox even: the thread's two columns are one aligned float2
+    const bool pair = (y_w & 1) == 0 && ((e.noise_nstride & 1) == 0) &&
+                      (((uintptr_t)y | (uintptr_t)e.u_save | (uintptr_t)e.noise) & 7) == 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int oy = oy0 + 4 * ty + i;
         if (oy >= y_h) continue;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int ox = ox0 + 2 * tx + j;
-            if (ox >= y_w) continue;
-            const int64_t pix = (int64_t)oy * y_w + ox;
-            const float u = out[i][j];
+        const int64_t pix = (int64_t)oy * y_w + ox;
+        if (pair) {
+            const float2 u2 = make_float2(out[i][0], out[i][1]);
             if (e.mode == SMC_EPI_STORE) {
-                y[plane + pix] = u;
+                *reinterpret_cast<float2*>(y + plane + pix) = u2;
                 continue;
             }
-            if (e.u_save) e.u_save[plane + pix] = u;
-            const float nz = e.noise ? e.noise[n * e.noise_nstride + pix] * nstr : 0.f;
-            y[plane + pix] = smc::epi_y(u, dv, nz, bv, e.act, e.alpha, e.gain, e.clamp);
+            if (e.u_save) *reinterpret_cast<float2*>(e.u_save + plane + pix) = u2;
+            float2 nz = make_float2(0.f, 0.f);
+            if (e.noise) {
+                nz = *reinterpret_cast<const float2*>(e.noise + n * e.noise_nstride + pix);
+                nz.x *= nstr;
+                nz.y *= nstr;
+            }
+            *reinterpret_cast<float2*>(y + plane + pix) =
+                make_float2(smc::epi_y(u2.x, dv, nz.x, bv, e.act, e.alpha, e.gain, e.clamp),
+                            smc::epi_y(u2.y, dv, nz.y, bv, e.act, e.alpha, e.gain, e.clamp));
+            continue;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (ox + j >= y_w) continue;
+            const float u = out[i][j];
+            if (e.mode == SMC_EPI_STORE) {
+                y[plane + pix + j] = u;
+                continue;
+            }
+            if (e.u_save) e.u_save[plane + pix + j] = u;
+            const float nz = e.noise ? e.noise[n * e.noise_nstride + pix + j] * nstr : 0.f;
+            y[plane + pix + j] = smc::epi_y(u, dv, nz, bv, e.act, e.alpha, e.gain, e.clamp);
         }
     }
 }
@@ -262,20 +303,37 @@ __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const f
     const int iy0 = oy0 - pady0, ix0 = ox0 - padx0;
     const int64_t uplane = nc * (int64_t)u_h * u_w;
     float part = 0.f;
-    for (int i = tid; i < ROWS * COLS; i += 256) {
+    // fixed-trip unrolled loads (u, g, noise of every element in flight at once), then the math
+    constexpr int NL = (ROWS * COLS + 255) / 256;
+    float uv[NL], gv[NL], nv[NL];
+    const float* up = u + uplane;
+    const float* gp = g + uplane;
+    const float* np_ = e.noise ? e.noise + n * e.noise_nstride : nullptr;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        const int i = tid + 256 * l;
         const int r = i / COLS, cc = i - r * COLS;
         const int iy = iy0 + r, ix = ix0 + cc;
+        const bool ok = i < ROWS * COLS && iy >= 0 && iy < u_h && ix >= 0 && ix < u_w;
+        const int pix = ok ? iy * u_w + ix : 0;
+        uv[l] = up[pix];
+        gv[l] = gp[pix];
+        nv[l] = np_ ? np_[pix] : 0.f;
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        const int i = tid + 256 * l;
+        const int r = i / COLS, cc = i - r * COLS;
+        const int iy = iy0 + r, ix = ix0 + cc;
+        const bool ok = i < ROWS * COLS && iy >= 0 && iy < u_h && ix >= 0 && ix < u_w;
         float v = 0.f;
-        if (iy >= 0 && iy < u_h && ix >= 0 && ix < u_w) {
-            const int64_t pix = (int64_t)iy * u_w + ix;
-            const float uv = u[uplane + pix];
-            const float nz = e.noise ? e.noise[n * e.noise_nstride + pix] * nstr : 0.f;
-            const float yv = smc::epi_y(uv, dv, nz, bv, e.act, e.alpha, e.gain, e.clamp);
-            const float dz = smc::act_grad_y(e.act, g[uplane + pix], yv, e.alpha, e.gain, e.clamp);
+        if (ok) {
+            const float yv = smc::epi_y(uv[l], dv, nv[l] * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
+            const float dz = smc::act_grad_y(e.act, gv[l], yv, e.alpha, e.gain, e.clamp);
             v = dz * dv;
-            if (iy >= oy0 && iy < oy0 + kFH && ix >= ox0 && ix < ox0 + kFW) part += dz * uv;
+            if (iy >= oy0 && iy < oy0 + kFH && ix >= ox0 && ix < ox0 + kFW) part += dz * uv[l];
         }
-        tile[r * STRIDE + cc] = v;
+        if (i < ROWS * COLS) tile[r * STRIDE + cc] = v;
     }
     __syncthreads();
     float out[4][2];
@@ -335,6 +393,55 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const float* g, const floa
         const float dz = smc::act_grad_y(e.act, g[base + p], yv, e.alpha, e.gain, e.clamp);
         du[base + p] = dz * dv;
         part += dz * uv;
+    }
+    if (dd) {
+        const float tot = block_sum256(part, red);
+        if (threadIdx.x == 0) atomicAdd(dd + nc, tot);
+    }
+}
+
+// float4 form (hw % 4 == 0): each thread owns AB_V float4 groups of one plane, all loads issued first.
+constexpr int AB_V = 4;
+__global__ __launch_bounds__(256) void act_bwd_vec4_kernel(const float* g, const float* u, float* du, float* dd, int c,
+                                                           int64_t hw, Epi e) {
+    __shared__ float red[4];
+    const int64_t nc = blockIdx.y;
+    const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
+    const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
+    const float dv = e.d ? e.d[nc] : 1.f;
+    const float bv = e.bias ? e.bias[o] : 0.f;
+    const int64_t hw4 = hw >> 2;
+    const float4* g4 = reinterpret_cast<const float4*>(g + nc * hw);
+    const float4* u4 = reinterpret_cast<const float4*>(u + nc * hw);
+    const float4* n4 = e.noise ? reinterpret_cast<const float4*>(e.noise + n * e.noise_nstride) : nullptr;
+    float4* du4 = reinterpret_cast<float4*>(du + nc * hw);
+    float part = 0.f;
+    const int64_t q0 = (int64_t)blockIdx.x * 256 * AB_V + threadIdx.x;
+    float4 gv[AB_V], uv[AB_V], nv[AB_V];
+#pragma unroll
+    for (int k = 0; k < AB_V; ++k) {
+        const int64_t q = q0 + 256 * k;
+        const int64_t qq = q < hw4 ? q : 0;
+        gv[k] = g4[qq];
+        uv[k] = u4[qq];
+        nv[k] = n4 ? n4[qq] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < AB_V; ++k) {
+        const int64_t q = q0 + 256 * k;
+        if (q >= hw4) continue;
+        const float ua[4] = {uv[k].x, uv[k].y, uv[k].z, uv[k].w};
+        const float ga[4] = {gv[k].x, gv[k].y, gv[k].z, gv[k].w};
+        const float na[4] = {nv[k].x, nv[k].y, nv[k].z, nv[k].w};
+        float r[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float yv = smc::epi_y(ua[j], dv, na[j] * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
+            const float dz = smc::act_grad_y(e.act, ga[j], yv, e.alpha, e.gain, e.clamp);
+            r[j] = dz * dv;
+            part += dz * ua[j];
+        }
+        du4[q] = make_float4(r[0], r[1], r[2], r[3]);
     }
     if (dd) {
         const float tot = block_sum256(part, red);
@@ -445,6 +552,13 @@ SMC_API int smc_modconv_act_bwd_f32(const float* g, const float* u, float* du, f
     SMC_CHECK(epi && epi->mode == SMC_EPI_MODACT, "smc_modconv_act_bwd_f32: needs a MODACT epilogue");
     const int64_t hw = (int64_t)h * w;
     const int64_t planes = (int64_t)n * c;
+    const uintptr_t align = (uintptr_t)g | (uintptr_t)u | (uintptr_t)du | (uintptr_t)epi->noise;
+    if (hw % 4 == 0 && (!epi->noise || epi->noise_nstride % 4 == 0) && align % 16 == 0) {
+        SMC_CHECK(planes < 65536, "smc_modconv_act_bwd_f32: too many planes");
+        hipLaunchKernelGGL(act_bwd_vec4_kernel, dim3((unsigned)smc::ceil_div(hw / 4, 256 * AB_V), (unsigned)planes),
+                           dim3(256), 0, smc::as_stream(stream), g, u, du, dd, c, hw, to_epi(epi));
+        return smc::check_launch("smc_modconv_act_bwd_f32");
+    }
     int64_t per_plane = smc::ceil_div(hw, 256 * 8);  // ~8 elements per thread
     if (per_plane < 1) per_plane = 1;
     SMC_CHECK(planes < 65536, "smc_modconv_act_bwd_f32: too many planes");

@@ -90,6 +90,9 @@ class DirectionFinder:
         self.it = 0
         T = S_TRAINABLE_SPACE_CHANNELS
         self.styles_direction = torch.zeros(1, N_STYLE_CHANNELS, 512, device=self.device)
+        # device-resident row index: indexing with the Python list would copy a host index tensor to the
+        # GPU on every use, a blocking copy that drains the stream mid-step
+        self.t_idx = torch.tensor(T, dtype=torch.long, device=self.device)
         self.delta = self.styles_direction[:, T].clone()
         if init_delta is not None:
             self.delta = init_delta.detach().to(self.device, torch.float32).reshape(1, len(T), 512).clone()
@@ -167,7 +170,7 @@ class DirectionFinder:
 
     def _finish(self, styles, d, id_terms, clip_terms, denom):
         T = S_TRAINABLE_SPACE_CHANNELS
-        sT = styles[:, T]
+        sT = styles.index_select(1, self.t_idx)
         l2_sum = ((sT + d) - sT).square().sum()
         id_part = self.coef["id"] * id_terms.sum() / denom
         clip_part = self.coef["clip"] * clip_terms.sum() / denom
@@ -188,7 +191,7 @@ class DirectionFinder:
         i = self.rng.randint(0, self.num_batches)
         lo, hi = i * self.B, min((i + 1) * self.B, self.n_items)
         a, b = _dist.shard_rows(lo, hi, self.world.rank, self.world.world_size)
-        self.styles_direction[:, S_TRAINABLE_SPACE_CHANNELS] = self.delta
+        self.styles_direction.index_copy_(1, self.t_idx, self.delta)
         buf = torch.zeros(self.delta.numel() + 4, device=self.device)
         if b > a:
             g, parts = self._local_terms(self.styles_array[a:b], hi - lo)

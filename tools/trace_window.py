@@ -48,7 +48,7 @@ def main():
         key = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:100]
         per_k[key] += e - s
         cnt[key] += 1
-    for k, t in per_k.most_common(25):
+    for k, t in per_k.most_common(int(sys.argv[5]) if len(sys.argv) > 5 else 25):
         print(f"  {t / 1e6 / steps:7.3f} ms/step  {cnt[k] / steps:6.1f} calls  {k}")
 
 
