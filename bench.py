@@ -25,7 +25,8 @@ profiles/pmc_traffic.json (null if absent).
 
 cpu_baseline (rank 0, N=1): the test oracle (pure-torch fp32 CPU restatement of the reference
 algorithm, oracle/) running the same step at FFHQ-1024 with batch 1 for --cpu-iters iterations on
---cpu-threads host threads.
+--cpu-threads host threads.  parity (same run): the GPU path repeats that exact oracle run and reports
+the cosine similarity of the two final directions (the metric's "dir cosine-sim vs ref").
 """
 import argparse
 import json
@@ -91,12 +92,33 @@ def cpu_baseline(resolution, iters, threads):
     net.requires_grad_(False)
     styles = synthetic.synthetic_styles(iters, seed=0)
     t0 = time.perf_counter()
-    OF.find_direction(G, styles, clip, OL.IDLoss(net), shapes, int(resolution).bit_length() - 3, batch_size=1,
-                      n_epochs=1, max_iterations=iters, init_delta=initial_delta(0, 0.01))
+    _, delta = OF.find_direction(G, styles, clip, OL.IDLoss(net), shapes, int(resolution).bit_length() - 3,
+                                 batch_size=1, n_epochs=1, max_iterations=iters, init_delta=initial_delta(0, 0.01))
     dt = time.perf_counter() - t0
     return {"value": 2 * iters / dt, "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{iters} find_direction iterations x 1 seed (FFHQ-{resolution}, CLIP ViT-B/32 + IR-SE50) "
-                      f"in {dt:.1f} s, oracle/ pure-torch fp32 CPU restatement, {threads} threads"}
+                      f"in {dt:.1f} s, oracle/ pure-torch fp32 CPU restatement, {threads} threads"}, delta.detach()
+
+
+def direction_parity(G, clip, id_loss, resolution, iters, delta_ref, dev, temp_shapes):
+    """The metric's 'dir cosine-sim vs ref': the GPU DirectionFinder run on the cpu_baseline's exact
+    problem (same seeded weights, the same `iters` S codes at batch 1, same batch picks and start point)
+    and its final direction compared with the oracle's."""
+    from stylemc_amd import synthetic
+    from stylemc_amd.find_direction import DirectionFinder, initial_delta
+    styles = synthetic.synthetic_styles(iters, seed=0).to(dev)
+    f = DirectionFinder(G, styles, clip, id_loss, resolution=resolution, batch_size=1, n_epochs=1, seed=0,
+                        init_delta=initial_delta(0, 0.01), temp_shapes=temp_shapes)
+    for _ in range(iters):
+        f.step()
+    g = f.delta.detach().cpu().double().flatten()
+    r = delta_ref.double().flatten()
+    cos = torch.nn.functional.cosine_similarity(g, r, dim=0).item()
+    err = ((g - r).abs().max() / r.abs().max()).item()
+    return {"dir_cosine_vs_oracle": round(cos, 7), "dir_max_rel_err": float(f"{err:.3e}"), "iters": iters,
+            "batch": 1, "target": ">= 0.999",
+            "what": f"final [1,8,512] direction after {iters} find_direction iterations at FFHQ-{resolution}: "
+                    f"HIP path vs oracle/ (fp32 CPU restatement of the reference loop) on identical inputs"}
 
 
 def pmc_traffic():
@@ -206,10 +228,16 @@ def main():
                    "direction_finite": finite},
         "roofline": roofline,
         "cpu_baseline": None,
+        "parity": None,
     }
     if world.world_size == 1 and not args.no_cpu_baseline:
         threads = min(args.cpu_threads, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(args.resolution, args.cpu_iters, threads)
+        out["cpu_baseline"], delta_ref = cpu_baseline(args.resolution, args.cpu_iters, threads)
+        try:
+            out["parity"] = direction_parity(G, clip, finder.id_loss, args.resolution, args.cpu_iters, delta_ref, dev,
+                                             finder.temp_shapes)
+        except Exception as e:  # keep the bench line; the failure is reported in it
+            out["parity"] = {"error": f"{type(e).__name__}: {e}"}
     print(json.dumps(out), flush=True)
 
 

@@ -58,6 +58,7 @@ struct GemmParams {
     smc::EpiExt ext;
     int nsplit;
     int64_t split_stride;
+    int per_sample;  // LDS-DMA kernel: blockIdx.x -> (sample, tile of that sample): no tile straddles two images
 };
 
 // Epilogue shared by the gather-GEMM kernels: lane owns column m, registers walk output channels.
@@ -335,8 +336,16 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_lds_kernel(GemmParams p) {
     const int split = blockIdx.z - phase * p.nsplit;
     const PhaseDev& ph = p.ph[phase];
     const int hw_out = ph.out_h * ph.out_w;
-    const int M = p.n * hw_out;
-    const int m0 = blockIdx.x * BM;
+    int M = p.n * hw_out;
+    int m0 = blockIdx.x * BM;
+    if (p.per_sample) {
+        // per-sample weights with hw_out % BM != 0: tiles restart at every image (M = that image's end)
+        const int tps = (hw_out + BM - 1) / BM;
+        const int nb = blockIdx.x / tps;
+        if (nb >= p.n) return;
+        m0 = nb * hw_out + (blockIdx.x - nb * tps) * BM;
+        M = (nb + 1) * hw_out;
+    }
     if (m0 >= M) return;
     const int o0 = blockIdx.y * BO;
     const int cpk = p.cin / BKT;
@@ -866,7 +875,7 @@ SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, 
     // whether it will be: reserve whenever the shape qualifies)
     bool scaled_ok = false;
     // (input size 1x1: the query reserves for a superset of the launches that use the area)
-    if (lds_shape_ok(n, cin, cout, 1, 1, phases, nphases, c, &scaled_ok) && scaled_ok)
+    if (lds_shape_ok(n, cin, cout, 1, 1, phases, nphases, c, &scaled_ok))
         bytes = ((bytes + 255) / 256) * 256 + wsample_floats(n, cin, cout, phases, nphases) * (int64_t)sizeof(float);
     return bytes;
 }
@@ -939,7 +948,22 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     dim3 grid((unsigned)smc::ceil_div(max_m, c.bm), (unsigned)smc::ceil_div(cout, c.bo), (unsigned)(nphases * nsplit));
     bool scaled_ok = false;
     const int nst = lds_stages(cfg);
-    if (nst && lds_shape_ok(n, cin, cout, in_h, in_w, phases, nphases, c, &scaled_ok) && (!s_in || scaled_ok)) {
+    // per-sample tiling pays where the per-sample weights are small next to the input planes (the
+    // high-resolution conv0 layers); on the 512-channel low-resolution layers writing n weight copies
+    // costs more than the register-staged kernel's in-loop scaling (tools/bench_gemm.py)
+    int taps_all = 0;
+    for (int i = 0; i < nphases; ++i) taps_all += phases[i].ntaps;
+    const bool small_w = (int64_t)taps_all * cout <= (int64_t)in_h * in_w;
+    if (nst && lds_shape_ok(n, cin, cout, in_h, in_w, phases, nphases, c, &scaled_ok) &&
+        (!s_in || scaled_ok || small_w)) {
+        if (s_in && !scaled_ok) {
+            // per-sample tiling: grid.x = n x (tiles of the largest phase image)
+            int64_t tps = 0;
+            for (int i = 0; i < nphases; ++i)
+                tps = std::max<int64_t>(tps, smc::ceil_div((int64_t)phases[i].out_h * phases[i].out_w, c.bm));
+            grid.x = (unsigned)(tps * n);
+            p.per_sample = 1;
+        }
         if (s_in) {
             // per-sample weights W[t][i][o] * s[n][i], [phase][n][taps*cin][cout], after the split-K partials
             const int64_t part = nsplit > 1 ? ((nsplit * plane_elems * (int64_t)sizeof(float) + 255) / 256) * 256 : 0;

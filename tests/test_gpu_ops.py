@@ -26,6 +26,23 @@ def close(a, b, tol, what=""):
     assert err <= tol * scale, f"{what}: max err {err:.3e} > {tol:.1e} * {scale:.3e}"
 
 
+def close_grad(a, b, tol, what="", max_flips=2):
+    """Gradient through lrelu/clamp: the activation mask is discontinuous, so an element whose
+    pre-activation sits within fp32 rounding of a kink (0, +-clamp) may legitimately take the other
+    branch (GPU and CPU accumulate the conv in different orders).  Those isolated elements are allowed
+    (at most `max_flips`, each still bounded by 1e-2 of the max); everything else must meet `tol`,
+    and the whole tensor must agree to `tol` in relative Frobenius norm."""
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    scale = max(b.abs().max().item(), 1e-12)
+    err = (a - b).abs()
+    bad = int((err > tol * scale).sum())
+    assert bad <= max_flips, f"{what}: {bad} elements beyond {tol:.1e} * {scale:.3e} (max {err.max():.3e})"
+    assert err.max().item() <= 1e-2 * scale, f"{what}: max err {err.max():.3e}"
+    rel = ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
+    assert rel <= tol, f"{what}: relative norm error {rel:.3e} > {tol:.1e}"
+
+
 @pytest.fixture(scope="module", autouse=True)
 def _gpu():
     if not torch.cuda.is_available():
@@ -159,8 +176,8 @@ def test_synthesis_layer_vs_oracle(cin, cout, res, up, n, noise_mode):
     yg = p(xg, sg, noise_mode=noise_mode)
     dxg, dsg = torch.autograd.grad((yg * cot.to(DEV)).sum(), [xg, sg])
     close(yg, yr, 2e-5, "y")
-    close(dxg, dxr, 1e-4, "dx")
-    close(dsg, dsr, 1e-4, "ds")
+    close_grad(dxg, dxr, 1e-4, "dx")
+    close_grad(dsg, dsr, 1e-4, "ds", max_flips=0)
 
 
 def test_synthesis_layer_grad_subsets():
