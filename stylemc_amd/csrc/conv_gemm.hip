@@ -830,6 +830,26 @@ bool lds_bk32(int cfg, int cin) {
     return on && cfg == 0 && cin % 32 == 0 && cin >= 512;
 }
 
+// 64x64 tile (4 waves of one 32x32 block each) for GEMMs whose cout-based tile leaves most CUs idle (the
+// IR-SE50 7..28-px stages, the synthesis 4..32-px blocks): 4x the workgroups before any split-K, so fewer
+// and shorter partial planes.  LDS-DMA kernel only; SMC_NO_SMALL_TILE=1 disables (A/B knob).
+bool small_tile_ok(int n, int cin, int cout, int in_h, int in_w, const smc_conv_phase* ph, int nph, bool has_s,
+                   const Cfg& base) {
+    static const bool off = getenv("SMC_NO_SMALL_TILE") != nullptr;
+    if (off || cout % 64 != 0 || lds_stages(1) == 0) return false;
+    int64_t blocks = 0;
+    int taps_all = 0;
+    for (int i = 0; i < nph; ++i) {
+        blocks += smc::ceil_div((int64_t)n * ph[i].out_h * ph[i].out_w, base.bm) * smc::ceil_div(cout, base.bo);
+        taps_all += ph[i].ntaps;
+    }
+    if (blocks >= smc::device_cu_count()) return false;
+    const Cfg sm{64, 64};
+    bool scaled_ok = false;
+    if (!lds_shape_ok(n, cin, cout, in_h, in_w, ph, nph, sm, &scaled_ok)) return false;
+    return !has_s || scaled_ok || (int64_t)taps_all * cout <= (int64_t)in_h * in_w;
+}
+
 int validate(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h, int y_w,
              const smc_conv_phase* phases, int nphases) {
     SMC_CHECK(x && y && phases, "smc_conv_gemm_f32: null pointer");
@@ -870,6 +890,7 @@ SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, 
         s = plan_split_convt(n, cin, cout, (y_h - 1) / 2, (y_w - 1) / 2);
     else
         s = plan_split(n, cin, cout, phases, nphases, c);
+    if (cout % 64 == 0) s = std::max(s, plan_split(n, cin, cout, phases, nphases, Cfg{64, 64}));  // small tile
     int64_t bytes = s > 1 ? (int64_t)s * n * cout * y_h * y_w * (int64_t)sizeof(float) : 0;
     // the LDS-DMA kernel's per-sample weights when the input is style-scaled (the query does not know
     // whether it will be: reserve whenever the shape qualifies)
@@ -888,9 +909,13 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     int rc = validate(x, n, cin, in_h, in_w, y, cout, y_h, y_w, phases, nphases);
     if (rc != SMC_OK) return rc;
     Cfg c;
-    const int cfg = pick_cfg(cout, &c);
+    int cfg = pick_cfg(cout, &c);
     ConvTParams ctp{};
     const bool fused_t = convt_fusable(cin, cout, in_h, in_w, y_h, y_w, phases, nphases, epi, &ctp);
+    if (!fused_t && small_tile_ok(n, cin, cout, in_h, in_w, phases, nphases, s_in != nullptr, c)) {
+        cfg = 3;
+        c = Cfg{64, 64};
+    }
     const int nsplit = fused_t ? plan_split_convt(n, cin, cout, in_h, in_w) : plan_split(n, cin, cout, phases, nphases, c);
     const int64_t plane_elems = (int64_t)n * cout * y_h * y_w;
     if (nsplit > 1) {
@@ -998,6 +1023,7 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             hipLaunchKernelGGL((conv_gemm_lds_kernel<2, 2, 2, 2, 32, 2>), grid, dim3(NT), 0, st, p);
         else if (cfg == 0) SMC_LAUNCH_LDS(2, 2, 2, 2);
         else if (cfg == 1) SMC_LAUNCH_LDS(1, 4, 2, 2);
+        else if (cfg == 3) SMC_LAUNCH_LDS(2, 2, 1, 1);
         else SMC_LAUNCH_LDS(1, 4, 1, 2);
 #undef SMC_LAUNCH_LDS
         rc = smc::check_launch("smc_conv_gemm_f32 (LDS-DMA)");
