@@ -843,7 +843,14 @@ bool small_tile_ok(int n, int cin, int cout, int in_h, int in_w, const smc_conv_
         blocks += smc::ceil_div((int64_t)n * ph[i].out_h * ph[i].out_w, base.bm) * smc::ceil_div(cout, base.bo);
         taps_all += ph[i].ntaps;
     }
-    if (blocks >= smc::device_cu_count()) return false;
+    // threshold measured on the FFHQ-1024 / IR-SE50 shapes (tools/bench_gemm.py, tools/prof_irse.py): the
+    // 128x128 tile with split-K stays ahead from 128 tiles up (r = 32 conv1); below that the 64x64 tile wins on
+    // the sum (synthesis GEMMs 12.14 ms at 128 vs 12.30 at 256; IR-SE50 pair 4.85 vs 5.06 ms at 32)
+    static const int64_t max_blocks = [] {
+        const char* f = getenv("SMC_SMALL_TILE_MAX_BLOCKS");
+        return f ? (int64_t)atoll(f) : (int64_t)128;
+    }();
+    if (blocks >= max_blocks) return false;
     const Cfg sm{64, 64};
     bool scaled_ok = false;
     if (!lds_shape_ok(n, cin, cout, in_h, in_w, ph, nph, sm, &scaled_ok)) return false;
