@@ -138,6 +138,98 @@ __global__ __launch_bounds__(256) void torgb_bwd_kernel(const float* g, const fl
     }
 }
 
+// Low-resolution forms (hw <= kSmallHw: the 4..64-px blocks, 512 input channels).  The per-position kernels
+// above give each thread the whole channel reduction, which at these sizes is 1-4 workgroups per image and a
+// chain of 64 dependent load rounds (~90 us for 16 positions).  Here the channels are split over the
+// workgroup and over more workgroups: forward = 16 positions x 16 channel groups per workgroup + an LDS
+// reduction; backward (no reduction over input channels) = 64 positions x 4 channel lanes, KCH channels per
+// workgroup in grid.y.
+constexpr int64_t kSmallHw = 4096;
+constexpr int kFwdP = 16, kFwdG = 16;
+constexpr int kBwdP = 64, kBwdKCH = 32;
+
+__global__ __launch_bounds__(256) void torgb_fwd_small_kernel(const float* x, const float* w, const float* s,
+                                                              const float* b, float* y, int cin, int cout, int64_t hw,
+                                                              float clamp) {
+    __shared__ float red[kFwdG][kMaxOut][kFwdP];
+    const int nn = blockIdx.y;
+    const int pl = threadIdx.x % kFwdP, grp = threadIdx.x / kFwdP;
+    const int64_t p = (int64_t)blockIdx.x * kFwdP + pl;
+    const bool pv = p < hw;
+    const float* xp = x + (int64_t)nn * cin * hw + (pv ? p : 0);
+    const float* sp = s + (int64_t)nn * cin;
+    float acc[kMaxOut] = {0.f, 0.f, 0.f, 0.f};
+    constexpr int U = 8;
+    int k = grp;
+    for (; k + (U - 1) * kFwdG < cin; k += U * kFwdG) {
+        float xv[U], sv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            xv[u] = xp[(int64_t)(k + u * kFwdG) * hw];
+            sv[u] = sp[k + u * kFwdG];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < kMaxOut; ++c) {
+                if (c >= cout) break;
+                acc[c] += (w[c * cin + k + u * kFwdG] * sv[u]) * xv[u];
+            }
+    }
+    for (; k < cin; k += kFwdG) {
+        const float xv = xp[(int64_t)k * hw];
+#pragma unroll
+        for (int c = 0; c < kMaxOut; ++c) {
+            if (c >= cout) break;
+            acc[c] += (w[c * cin + k] * sp[k]) * xv;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < kMaxOut; ++c) red[grp][c][pl] = acc[c];
+    __syncthreads();
+    if (threadIdx.x < kMaxOut * kFwdP) {
+        const int c = threadIdx.x / kFwdP, q = threadIdx.x % kFwdP;
+        const int64_t pp = (int64_t)blockIdx.x * kFwdP + q;
+        if (c < cout && pp < hw) {
+            float t = 0.f;
+#pragma unroll
+            for (int g2 = 0; g2 < kFwdG; ++g2) t += red[g2][c][q];
+            y[((int64_t)nn * cout + c) * hw + pp] = smc::clamp_fwd(t + (b ? b[c] : 0.f), clamp);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void torgb_bwd_small_kernel(const float* g, const float* y, const float* w,
+                                                              const float* s, float* dx, int cin, int cout, int64_t hw,
+                                                              float clamp, int scale, int accumulate) {
+    const int nn = blockIdx.z;
+    const int pl = threadIdx.x % kBwdP, kl = threadIdx.x / kBwdP;
+    const int64_t p = (int64_t)blockIdx.x * kBwdP + pl;
+    if (p >= hw) return;
+    float gm[kMaxOut];
+#pragma unroll
+    for (int c = 0; c < kMaxOut; ++c) {
+        gm[c] = 0.f;
+        if (c >= cout) continue;
+        const int64_t off = ((int64_t)nn * cout + c) * hw + p;
+        const float yv = y[off];
+        const bool pass = clamp < 0.f || (yv > -clamp && yv < clamp);  // bias_act.cu:136-141 (grad=1)
+        gm[c] = pass ? g[off] : 0.f;
+    }
+    const int k0 = blockIdx.y * kBwdKCH;
+    for (int k = k0 + kl; k < k0 + kBwdKCH && k < cin; k += 256 / kBwdP) {
+        const float sk = scale ? s[(int64_t)nn * cin + k] : 1.f;
+        float r = 0.f;
+#pragma unroll
+        for (int c = 0; c < kMaxOut; ++c) {
+            if (c >= cout) break;
+            r += (w[c * cin + k] * sk) * gm[c];
+        }
+        float* dst = dx + ((int64_t)nn * cin + k) * hw + p;
+        *dst = accumulate ? *dst + r : r;
+    }
+}
+
 }  // namespace
 
 SMC_API int smc_torgb_fwd_f32(const float* x, const float* w, const float* s, const float* b, float* y, int n, int cin,
@@ -149,6 +241,11 @@ SMC_API int smc_torgb_fwd_f32(const float* x, const float* w, const float* s, co
         return SMC_ERR_UNSUPPORTED;
     }
     const int64_t hw = (int64_t)h * w_;
+    if (hw <= kSmallHw) {
+        hipLaunchKernelGGL(torgb_fwd_small_kernel, dim3((unsigned)smc::ceil_div(hw, kFwdP), (unsigned)n), dim3(256), 0,
+                           smc::as_stream(stream), x, w, s, b, y, cin, cout, hw, clamp);
+        return smc::check_launch("smc_torgb_fwd_f32");
+    }
     const bool vec = hw % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
     const int64_t per = vec ? hw / 4 : hw;
     dim3 grid((unsigned)smc::ceil_div(per, 256), (unsigned)n);
@@ -169,6 +266,12 @@ SMC_API int smc_torgb_bwd_f32(const float* g, const float* y, const float* w, co
         return SMC_ERR_UNSUPPORTED;
     }
     const int64_t hw = (int64_t)h * w_;
+    if (hw <= kSmallHw) {
+        dim3 grid((unsigned)smc::ceil_div(hw, kBwdP), (unsigned)smc::ceil_div(cin, kBwdKCH), (unsigned)n);
+        hipLaunchKernelGGL(torgb_bwd_small_kernel, grid, dim3(256), 0, smc::as_stream(stream), g, y, w, s, dx, cin,
+                           cout, hw, clamp, scale, accumulate);
+        return smc::check_launch("smc_torgb_bwd_f32");
+    }
     const bool vec = hw % 4 == 0 && (reinterpret_cast<uintptr_t>(dx) & 15) == 0;
     const int64_t per = vec ? hw / 4 : hw;
     dim3 grid((unsigned)smc::ceil_div(per, 256), (unsigned)n);
