@@ -1,0 +1,44 @@
+"""Cross-check bench.py's live roofline (HIP events around every smc_conv_gemm_f32 call of the serialised
+roofline pass) against the rocprofv3 kernel trace of the same run.
+
+    python tools/roofline_check.py run_kernel_trace.csv [launches=100]
+
+The roofline pass is the last `launches` synthesis-GEMM calls of the run.  One smc_conv_gemm_f32 call is
+the GEMM kernel (TAG 0) plus, where the layer needs them, the per-sample weight kernel launched right before
+it (wscale_kernel) and the split-K reduction launched right after it (epilogue_kernel); the HIP events
+bracket all of them, so both the kernel-only and the whole-call averages are printed."""
+import csv
+import sys
+
+
+def main():
+    path = sys.argv[1]
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    is_fam = lambda r: ("conv_gemm" in r["Kernel_Name"] or "convt_gemm_kernel" in r["Kernel_Name"]) and \
+        ", 1>(" not in r["Kernel_Name"]
+    idx = [i for i, r in enumerate(rows) if is_fam(r)][-n:]
+    dur = lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    k_tot = sum(dur(rows[i]) for i in idx)
+    call_tot = 0
+    for i in idx:
+        s, st = rows[i], rows[i]["Stream_Id"]
+        start, end = int(s["Start_Timestamp"]), int(s["End_Timestamp"])
+        j = i - 1
+        while j >= 0 and rows[j]["Stream_Id"] != st:
+            j -= 1
+        if j >= 0 and "wscale_kernel" in rows[j]["Kernel_Name"]:
+            start = int(rows[j]["Start_Timestamp"])
+        j = i + 1
+        while j < len(rows) and rows[j]["Stream_Id"] != st:
+            j += 1
+        if j < len(rows) and "epilogue_kernel(" in rows[j]["Kernel_Name"] and "lin_" not in rows[j]["Kernel_Name"]:
+            end = int(rows[j]["End_Timestamp"])
+        call_tot += end - start
+    print(f"last {len(idx)} synthesis GEMM launches (serialised roofline pass): kernel-only average "
+          f"{k_tot / len(idx) / 1e3:.1f} us, whole smc_conv_gemm_f32 call (wscale + GEMM + split-K reduce, "
+          f"first start to last end) {call_tot / len(idx) / 1e3:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
