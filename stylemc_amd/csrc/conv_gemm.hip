@@ -59,6 +59,7 @@ struct GemmParams {
     int nsplit;
     int64_t split_stride;
     int per_sample;  // LDS-DMA kernel: blockIdx.x -> (sample, tile of that sample): no tile straddles two images
+    int ntn;         // LDS-DMA kernel: column tiles; grid.x = row tiles x ntn, XCD-swizzled (0: 2-D grid)
 };
 
 // Epilogue shared by the gather-GEMM kernels: lane owns column m, registers walk output channels.
@@ -336,18 +337,30 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_lds_kernel(GemmParams p) {
     const int split = blockIdx.z - phase * p.nsplit;
     const PhaseDev& ph = p.ph[phase];
     const int hw_out = ph.out_h * ph.out_w;
+    // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (private L2 each), so the
+    // bijective remap below gives every XCD a contiguous run of tiles, column tiles fastest: the workgroups
+    // that share an input tile (all column tiles of one row tile) and the row-neighbour tiles the 3x3 taps
+    // re-read run on the same L2.
+    int tm = blockIdx.x, tn = blockIdx.y;
+    if (p.ntn) {
+        const int nwg = gridDim.x, orig = blockIdx.x;
+        const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+        const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+        tm = wgid / p.ntn;
+        tn = wgid - tm * p.ntn;
+    }
     int M = p.n * hw_out;
-    int m0 = blockIdx.x * BM;
+    int m0 = tm * BM;
     if (p.per_sample) {
         // per-sample weights with hw_out % BM != 0: tiles restart at every image (M = that image's end)
         const int tps = (hw_out + BM - 1) / BM;
-        const int nb = blockIdx.x / tps;
+        const int nb = tm / tps;
         if (nb >= p.n) return;
-        m0 = nb * hw_out + (blockIdx.x - nb * tps) * BM;
+        m0 = nb * hw_out + (tm - nb * tps) * BM;
         M = (nb + 1) * hw_out;
     }
     if (m0 >= M) return;
-    const int o0 = blockIdx.y * BO;
+    const int o0 = tn * BO;
     const int cpk = p.cin / BKT;
     const int ks_total = ph.ntaps * cpk;
     const int ks_begin = (int)((int64_t)ks_total * split / p.nsplit);
@@ -432,33 +445,43 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_lds_kernel(GemmParams p) {
         }
         __builtin_amdgcn_s_barrier();  // every wave's DMAs for step ks have landed; slot ks-1 is free
         asm volatile("" ::: "memory");
-        if (issued < ks_end) {
-            issue(issued, (issued - ks_begin) % NST);
-            ++issued;
-        }
         const int slot = (ks - ks_begin) % NST;
         const float* Ws = smem + slot * TILE;
         const float* Xs = Ws + BKT * BO;
         const float* wrow = Ws + kh * BO + wo * TO * 32 + l32;
         const float* xrow = Xs + kh * BM + wm * TM * 32 + l32;
+        // Step schedule: the workgroups sharing a CU run in near lockstep, so whatever a wave does between
+        // the barrier and its first MFMA leaves the SIMD's MFMA pipe idle for every wave at once.  Only the
+        // first half-chunk of fragment reads precedes the first MFMAs; the DMA issue for a later step and
+        // the second half of the reads are issued under the executing MFMAs.
 #pragma unroll
         for (int k0 = 0; k0 < BKT; k0 += 16) {
             float af[8][TO], bf[8][TM];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
+            auto frag = [&](int q) {
 #pragma unroll
                 for (int i = 0; i < TO; ++i) af[q][i] = wrow[(k0 + 2 * q) * BO + i * 32];
 #pragma unroll
                 for (int j = 0; j < TM; ++j) bf[q][j] = xrow[(k0 + 2 * q) * BM + j * 32];
-            }
-            __builtin_amdgcn_sched_barrier(0);  // fragment reads first: the LDS latency is paid once per chunk
+            };
+            // software pipeline over the 8 K-pairs: fragments of pair q+2 are read under pair q's MFMAs
+            frag(0);
+            frag(1);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
+            for (int q = 0; q < 8; ++q) {
 #pragma unroll
                 for (int i = 0; i < TO; ++i)
 #pragma unroll
                     for (int j = 0; j < TM; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q][i], bf[q][j], acc[i][j], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (q == 0 && k0 == 0 && issued < ks_end) {
+                    issue(issued, (issued - ks_begin) % NST);
+                    ++issued;
+                }
+                if (q + 2 < 8) frag(q + 2);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragment reads of this slot done before the next barrier
     }
@@ -1017,6 +1040,12 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             if (rc != SMC_OK) return rc;
         }
         p.s = nullptr;
+        static const bool no_swz = getenv("SMC_NO_XCD_SWIZZLE") != nullptr;  // A/B knob
+        if (!no_swz) {
+            p.ntn = (int)grid.y;
+            grid.x *= grid.y;
+            grid.y = 1;
+        }
 #define SMC_LAUNCH_LDS(WO_, WM_, TO_, TM_)                                                                          \
     do {                                                                                                          \
         if (nst == 2 && tag) hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 2, 1>), grid, dim3(NT), 0, st, p); \
