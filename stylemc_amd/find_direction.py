@@ -132,11 +132,22 @@ class DirectionFinder:
             img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
             with torch.no_grad():
                 orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
-        id_terms = self.id_loss.per_sample_pair(img, orig)
+        if side is not None:
+            # the two loss networks are independent and neither fills the GPU (small GEMMs): IR-SE50 runs on
+            # the second stream beside CLIP; autograd runs each backward on its forward's stream and joins
+            # them where the gradients meet (d img)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                id_terms = self.id_loss.per_sample_pair(img, orig)
+        else:
+            id_terms = self.id_loss.per_sample_pair(img, orig)
         tgt = unprocess(img, self.mean, self.std)
         with torch.no_grad():
             src = unprocess(orig, self.mean, self.std)
         clip_terms = sum(w * cl.per_sample_pair(tgt, src) for cl, w in self.clip_losses)
+        if side is not None:
+            main.wait_stream(side)
+            id_terms.record_stream(main)
         return id_terms, clip_terms
 
     def _local_terms(self, styles, denom):
