@@ -488,6 +488,20 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_lds_kernel(GemmParams p) {
     gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32);
 }
 
+// Style-scaled input for the low-resolution layers: out[n][i][p] = x[n][i][p] * s[n][i] (float4 when hw % 4 == 0).
+__global__ __launch_bounds__(256) void xscale_kernel(const float* x, const float* s, float* out, int64_t hw,
+                                                     int64_t planes) {
+    const int64_t per = hw / 4;
+    const int64_t total = per * planes;
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < total; v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t pl = v / per;
+        const float sc = s[pl];
+        float4 a = reinterpret_cast<const float4*>(x)[v];
+        a.x *= sc; a.y *= sc; a.z *= sc; a.w *= sc;
+        reinterpret_cast<float4*>(out)[v] = a;
+    }
+}
+
 // Per-sample weights for the LDS-DMA kernel: out[n][row][o] = wk[row][o] * s[n][row % cin].
 __global__ __launch_bounds__(256) void wscale_kernel(const float* wk, const float* s, float* out, int rows, int cin,
                                                      int cout, int n) {
@@ -880,6 +894,22 @@ bool small_tile_ok(int n, int cin, int cout, int in_h, int in_w, const smc_conv_
     return !has_s || scaled_ok || (int64_t)taps_all * cout <= (int64_t)in_h * in_w;
 }
 
+// Input prescale (x * s into the workspace, then the shared-weight GEMM) replaces the per-sample weights
+// where the input is the smaller of the two: the 4..64-px layers (n*cin*hw < n*taps*cin*cout), which
+// otherwise write n copies of a 512x512x9 weight tensor (37.7 MB at n = 4) or fall back to the
+// register-staged kernel.  Returns the floats to reserve (0: not a prescale shape); stride-1 phases
+// only, the phase output images bounding the input image (3x3 same conv, 4-phase transposed conv).
+int64_t prescale_floats(int n, int cin, int cout, const smc_conv_phase* ph, int nph) {
+    int64_t hw = 0;
+    int taps_all = 0;
+    for (int i = 0; i < nph; ++i) {
+        if (ph[i].in_stride != 1) return 0;
+        hw = std::max<int64_t>(hw, (int64_t)ph[i].out_h * ph[i].out_w);
+        taps_all += ph[i].ntaps;
+    }
+    return hw <= (int64_t)taps_all * cout ? (((int64_t)n * cin * hw + 63) / 64) * 64 : 0;
+}
+
 int validate(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h, int y_w,
              const smc_conv_phase* phases, int nphases) {
     SMC_CHECK(x && y && phases, "smc_conv_gemm_f32: null pointer");
@@ -926,8 +956,10 @@ SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, 
     // whether it will be: reserve whenever the shape qualifies)
     bool scaled_ok = false;
     // (input size 1x1: the query reserves for a superset of the launches that use the area)
-    if (lds_shape_ok(n, cin, cout, 1, 1, phases, nphases, c, &scaled_ok))
-        bytes = ((bytes + 255) / 256) * 256 + wsample_floats(n, cin, cout, phases, nphases) * (int64_t)sizeof(float);
+    const int64_t pre = prescale_floats(n, cin, cout, phases, nphases);
+    if (lds_shape_ok(n, cin, cout, 1, 1, phases, nphases, c, &scaled_ok) || pre > 0)
+        bytes = ((bytes + 255) / 256) * 256 +
+                std::max(wsample_floats(n, cin, cout, phases, nphases), pre) * (int64_t)sizeof(float);
     return bytes;
 }
 
@@ -942,6 +974,12 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     int cfg = pick_cfg(cout, &c);
     ConvTParams ctp{};
     const bool fused_t = convt_fusable(cin, cout, in_h, in_w, y_h, y_w, phases, nphases, epi, &ctp);
+    static const bool no_pre = getenv("SMC_NO_PRESCALE") != nullptr;  // A/B knob
+    const int64_t pre_fl = prescale_floats(n, cin, cout, phases, nphases);
+    const bool prescale = s_in && !fused_t && !no_pre && pre_fl > 0 && (int64_t)n * cin * in_h * in_w <= pre_fl &&
+                          (in_h * in_w) % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    const float* s_prescale = s_in;
+    if (prescale) s_in = nullptr;  // the GEMM reads x * s from the workspace with the shared weights
     if (!fused_t && small_tile_ok(n, cin, cout, in_h, in_w, phases, nphases, s_in != nullptr, c)) {
         cfg = 3;
         c = Cfg{64, 64};
@@ -952,6 +990,20 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         const int64_t need = nsplit * plane_elems * (int64_t)sizeof(float);
         SMC_CHECK(workspace && workspace_bytes >= need, "smc_conv_gemm_f32: workspace %lld < %lld bytes",
                   (long long)workspace_bytes, (long long)need);
+    }
+    if (prescale) {
+        // x * s after the split-K partials (the query reserved max(per-sample weights, prescaled input))
+        const int64_t part = nsplit > 1 ? ((nsplit * plane_elems * (int64_t)sizeof(float) + 255) / 256) * 256 : 0;
+        const int64_t need = part + pre_fl * (int64_t)sizeof(float);
+        SMC_CHECK(workspace && workspace_bytes >= need, "smc_conv_gemm_f32: workspace %lld < %lld bytes",
+                  (long long)workspace_bytes, (long long)need);
+        float* xs = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + part);
+        const int64_t planes = (int64_t)n * cin, hw = (int64_t)in_h * in_w;
+        hipLaunchKernelGGL(xscale_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(planes * hw / 4, 256), 4096)),
+                           dim3(256), 0, smc::as_stream(stream), x, s_prescale, xs, hw, planes);
+        rc = smc::check_launch("smc_conv_gemm_f32 (prescaled input)");
+        if (rc != SMC_OK) return rc;
+        x = xs;
     }
     GemmParams p{};
     p.x = x; p.n = n; p.cin = cin; p.in_h = in_h; p.in_w = in_w;

@@ -111,5 +111,25 @@ def main():
         torch.cuda.empty_cache()
 
 
+
+
+def ufd_main():
+    """upsample2d / downsample2d of the 3-channel skip image (the skip-architecture img path)."""
+    from stylemc_amd.torch_utils.ops import upfirdn2d
+    f = upfirdn2d.setup_filter([1, 3, 3, 1], device="cuda")
+    for r in (1024, 512, 256):
+        img = torch.randn(4, 3, r // 2, r // 2, device="cuda")
+        us = timeit(lambda: upfirdn2d.upsample2d(img, f))
+        byt = 4 * (img.numel() + 4 * img.numel())
+        print(f"r={r:5d} upsample2d    {us:8.1f} us  {byt / us / 1e3:7.0f} GB/s")
+        big = torch.randn(4, 3, r, r, device="cuda")
+        us = timeit(lambda: upfirdn2d.downsample2d(big, f))
+        byt = 4 * (big.numel() + big.numel() // 4)
+        print(f"r={r:5d} downsample2d  {us:8.1f} us  {byt / us / 1e3:7.0f} GB/s")
+
+
 if __name__ == "__main__":
-    main()
+    if "--ufd" in sys.argv:
+        ufd_main()
+    else:
+        main()
