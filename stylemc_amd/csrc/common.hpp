@@ -38,11 +38,13 @@ __device__ __forceinline__ float clamp_fwd(float y, float clamp) {
 }
 
 // dz given the incoming gradient g and the forward output y.
+// bias_act.cu tests (yref / gain) > 0; the sign test below is the same predicate without the per-element
+// IEEE division (it differs only where y / gain underflows to zero, |y| < 2^-149 |gain|).
 __device__ __forceinline__ float act_grad_y(int act, float g, float y, float alpha, float gain, float clamp) {
-    float yy = gain != 0.f ? y / gain : 0.f;
+    const bool pos = gain > 0.f ? y > 0.f : (gain < 0.f ? y < 0.f : false);
     float r = g;
-    if (act == SMC_ACT_RELU) r = yy > 0.f ? g : 0.f;
-    if (act == SMC_ACT_LRELU) r = yy > 0.f ? g : g * alpha;
+    if (act == SMC_ACT_RELU) r = pos ? g : 0.f;
+    if (act == SMC_ACT_LRELU) r = pos ? g : g * alpha;
     r *= gain;
     if (clamp >= 0.f) r = (y > -clamp && y < clamp) ? r : 0.f;
     return r;

@@ -177,6 +177,32 @@ __device__ __forceinline__ void fir_block(const float* tile, int stride, int ly0
     }
 }
 
+// As fir_block, but the thread's two output columns are lx0 and lx0 + 32: a wave's store instruction then
+// covers 32 consecutive columns of two rows (two 128-B segments) instead of every other column.
+template <int FH, int FW>
+__device__ __forceinline__ void fir_block_split(const float* tile, int stride, int ly0, int lx0,
+                                                const float (&tp)[FH][FW], float (&out)[4][2]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i][0] = out[i][1] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4 + FH - 1; ++r) {
+        float v[2][FW];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int c = 0; c < FW; ++c) v[j][c] = tile[(ly0 + r) * stride + lx0 + 32 * j + c];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int jy = r - i;
+            if (jy < 0 || jy >= FH) continue;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int jx = 0; jx < FW; ++jx) out[i][j] += tp[jy][jx] * v[j][jx];
+        }
+    }
+}
+
 template <int FH, int FW>
 __device__ __forceinline__ void load_taps(const float* f, int flip, float fgain, float (&tp)[FH][FW]) {
 #pragma unroll
@@ -337,7 +363,7 @@ __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const f
     }
     __syncthreads();
     float out[4][2];
-    fir_block<FH, FW>(tile, STRIDE, 4 * ty, 2 * tx, tp, out);
+    fir_block_split<FH, FW>(tile, STRIDE, 4 * ty, tx, tp, out);
     const int64_t tplane = nc * (int64_t)t_h * t_w;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -345,7 +371,7 @@ __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const f
         if (oy >= t_h) continue;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int ox = ox0 + 2 * tx + j;
+            const int ox = ox0 + tx + 32 * j;
             if (ox < t_w) dt[tplane + (int64_t)oy * t_w + ox] = out[i][j];
         }
     }

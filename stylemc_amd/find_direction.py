@@ -64,10 +64,16 @@ class DirectionFinder:
     def __init__(self, G, styles_array, clip_losses, id_loss, resolution=1024, batch_size=4, learning_rate=1.5,
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
-                 overlap=True, batch_losses=True):
+                 overlap=True, batch_losses=True, prefetch_orig=True):
         self.G = G
         self.synth_fn = synth_fn or utils.generate_image_rows   # (G, until_k, styles, shapes, noise, delta=)
         self.overlap = overlap                                  # original-image branch on a second stream
+        # software pipelining across iterations: the NEXT iteration's original-image synthesis (it depends only
+        # on the S codes of the next batch, not on the direction) runs on a third stream during this
+        # iteration's backward; every iteration still synthesises its own original image exactly once
+        self.prefetch_orig = prefetch_orig
+        self._next_i = None
+        self._pref = None
         # edited + original image through each loss network as ONE batch (backward for the edited half)
         self.batch_losses = batch_losses and hasattr(id_loss, "per_sample_pair") and all(
             hasattr(cl, "per_sample_pair") for cl, _ in clip_losses)
@@ -116,11 +122,19 @@ class DirectionFinder:
             src_embs = [cl.encode_src(src) for cl, _ in self.clip_losses]
         return y_feats, src_embs
 
-    def _pair_terms(self, styles, d):
+    def _pair_terms(self, styles, d, key=None):
         """Batched-loss form: the original image's synthesis (no gradient) runs on the second stream
-        beside the edited one; then each loss network sees [edited; original] as one batch."""
+        beside the edited one (or was already run by the previous iteration's prefetch, `key` = its
+        rows); then each loss network sees [edited; original] as one batch."""
         side = self._side_stream()
-        if side is not None:
+        pref, self._pref = self._pref, None
+        if side is not None and pref is not None and pref[0] == key:
+            main = torch.cuda.current_stream()
+            img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+            main.wait_stream(self._pre)
+            orig = pref[1]
+            orig.record_stream(main)
+        elif side is not None:
             main = torch.cuda.current_stream()
             side.wait_stream(main)
             with torch.cuda.stream(side), torch.no_grad():
@@ -148,9 +162,11 @@ class DirectionFinder:
         if side is not None:
             main.wait_stream(side)
             id_terms.record_stream(main)
+            self._fwd_done = torch.cuda.Event()
+            self._fwd_done.record(main)
         return id_terms, clip_terms
 
-    def _local_terms(self, styles, denom):
+    def _local_terms(self, styles, denom, key=None):
         """Sum-form loss of this rank's shard: every per-sample term / global batch size.
 
         On the GPU the original-image branch runs on a second HIP stream, concurrently with the edited
@@ -159,7 +175,7 @@ class DirectionFinder:
         T = S_TRAINABLE_SPACE_CHANNELS
         d = self.delta.detach().clone().requires_grad_(True)
         if self.batch_losses:
-            id_terms, clip_terms = self._pair_terms(styles, d)
+            id_terms, clip_terms = self._pair_terms(styles, d, key)
             return self._finish(styles, d, id_terms, clip_terms, denom)
         side = self._side_stream()
         if side is not None:
@@ -196,18 +212,43 @@ class DirectionFinder:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
+    def _shard(self, i):
+        lo, hi = i * self.B, min((i + 1) * self.B, self.n_items)
+        return lo, hi, _dist.shard_rows(lo, hi, self.world.rank, self.world.world_size)
+
+    def _prefetch_next(self):
+        """Draw the next iteration's batch (the same single randint per iteration, one step early) and start
+        its original-image synthesis on the third stream once this iteration's forward is done."""
+        self._next_i = self.rng.randint(0, self.num_batches)
+        _, _, (a, b) = self._shard(self._next_i)
+        if b <= a:
+            return
+        if getattr(self, "_pre", None) is None:
+            self._pre = torch.cuda.Stream(device=self.device)
+        self._pre.wait_event(self._fwd_done)
+        with torch.cuda.stream(self._pre), torch.no_grad():
+            orig = self.synth_fn(self.G, self.until_k, self.styles_array[a:b], self.temp_shapes, self.noise_mode)
+        self._pref = ((a, b), orig)
+
     def step(self):
         self.it += 1
         lr_t = cosine_lr(self.lr0, self.it, self.total_iterations)
-        i = self.rng.randint(0, self.num_batches)
-        lo, hi = i * self.B, min((i + 1) * self.B, self.n_items)
-        a, b = _dist.shard_rows(lo, hi, self.world.rank, self.world.world_size)
+        if self._next_i is not None:
+            i, self._next_i = self._next_i, None
+        else:
+            i = self.rng.randint(0, self.num_batches)
+        lo, hi, (a, b) = self._shard(i)
         self.styles_direction.index_copy_(1, self.t_idx, self.delta)
         buf = torch.zeros(self.delta.numel() + 4, device=self.device)
+        pipelined = self.prefetch_orig and self.batch_losses and self._side_stream() is not None
         if b > a:
-            g, parts = self._local_terms(self.styles_array[a:b], hi - lo)
+            g, parts = self._local_terms(self.styles_array[a:b], hi - lo, key=(a, b))
             buf[:-4] = g.flatten()
             buf[-4:] = parts
+            if pipelined:
+                self._prefetch_next()
+        elif pipelined:
+            self._pref = None
         self.world.all_reduce_(buf)
         grad = buf[:-4].view_as(self.delta)
         self.delta = torch.add(self.delta, grad, alpha=-lr_t)  # == torch.optim.SGD step (find_direction.py:339)
