@@ -147,6 +147,10 @@ class DirectionFinder:
             with torch.no_grad():
                 orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
         if side is not None:
+            # the next iteration's original-image synthesis (prefetch stream) may start from here: it then
+            # overlaps the latency-bound loss networks and this iteration's backward
+            self._fwd_done = torch.cuda.Event()
+            self._fwd_done.record(main)
             # the two loss networks are independent and neither fills the GPU (small GEMMs): IR-SE50 runs on
             # the second stream beside CLIP; autograd runs each backward on its forward's stream and joins
             # them where the gradients meet (d img)
@@ -162,8 +166,6 @@ class DirectionFinder:
         if side is not None:
             main.wait_stream(side)
             id_terms.record_stream(main)
-            self._fwd_done = torch.cuda.Event()
-            self._fwd_done.record(main)
         return id_terms, clip_terms
 
     def _local_terms(self, styles, denom, key=None):
