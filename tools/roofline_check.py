@@ -27,7 +27,7 @@ def main():
         j = i - 1
         while j >= 0 and rows[j]["Stream_Id"] != st:
             j -= 1
-        if j >= 0 and "wscale_kernel" in rows[j]["Kernel_Name"]:
+        if j >= 0 and ("wscale_kernel" in rows[j]["Kernel_Name"] or "xscale_kernel" in rows[j]["Kernel_Name"]):
             start = int(rows[j]["Start_Timestamp"])
         j = i + 1
         while j < len(rows) and rows[j]["Stream_Id"] != st:
