@@ -272,14 +272,19 @@ class DirectionFinder:
 
 
 def load_generator(network, resolution, device):
-    """'synthetic' -> seeded config-f generator; *.pt/*.pth/*.safetensors -> state_dict (legacy.py:172-203 names)."""
-    from . import networks, synthetic
+    """'synthetic' -> seeded config-f generator; *.pkl -> the pickle's G_ema through the exec-free unpickler
+    (stylemc_amd.legacy); *.pt/*.pth/*.safetensors -> state_dict (legacy.py:172-203 names)."""
+    from . import legacy, networks, synthetic
     cfg = synthetic.generator_config(resolution=resolution)
     if network in (None, "", "synthetic"):
         return networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=device)
-    if network.endswith(".pkl") or network.startswith("http"):
-        raise SystemExit(f"{network}: network pickles execute embedded code on load and cannot be fetched "
-                         f"offline; convert G_ema to a state_dict (.pt) first")
+    if network.startswith("http"):
+        raise SystemExit(f"{network}: no network access; download the pickle and pass its local path")
+    if network.endswith(".pkl"):
+        G = legacy.load_generator_pkl(network, device=device)
+        if G.img_resolution != resolution:
+            raise SystemExit(f"{network}: generator resolution {G.img_resolution} != --resolution {resolution}")
+        return G
     if network.endswith(".safetensors"):
         from safetensors.torch import load_file
         sd = load_file(network)
