@@ -768,6 +768,10 @@ struct ConvTCfg {
 ConvTCfg convt_cfg(int cout) {
     if (cout % 128 == 0) return {128, 64, 0};
     if (cout % 64 == 0) return {64, 128, 1};
+    // 32 x 128 tile: 159 VGPR + 80 AGPR -> 2 workgroups per CU (the 32 x 256 tile's 256 + 160 allow one):
+    // 763 -> 620 us on the r = 1024 conv0 (tools/bench_gemm.py).  SMC_CONVT_BM=256 restores the wide tile.
+    static const int bm = getenv("SMC_CONVT_BM") ? atoi(getenv("SMC_CONVT_BM")) : 128;
+    if (bm == 128) return {32, 128, 3};
     return {32, 256, 2};
 }
 
@@ -1047,6 +1051,7 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         dim3 g((unsigned)smc::ceil_div(M, tc.bm), (unsigned)smc::ceil_div(cout, tc.bo), (unsigned)nsplit);
         if (tc.id == 0) hipLaunchKernelGGL((convt_gemm_kernel<2, 2, 2, 1, 16>), g, dim3(NT), 0, st, p, ctp);
         else if (tc.id == 1) hipLaunchKernelGGL((convt_gemm_kernel<1, 4, 2, 1, 16>), g, dim3(NT), 0, st, p, ctp);
+        else if (tc.id == 3) hipLaunchKernelGGL((convt_gemm_kernel<1, 4, 1, 1, 16>), g, dim3(NT), 0, st, p, ctp);
         else hipLaunchKernelGGL((convt_gemm_kernel<1, 4, 1, 2, 16>), g, dim3(NT), 0, st, p, ctp);
         rc = smc::check_launch("smc_conv_gemm_f32 (fused transposed conv)");
         if (rc != SMC_OK || nsplit == 1) return rc;
