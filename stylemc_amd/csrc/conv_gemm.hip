@@ -798,10 +798,21 @@ struct Cfg {
 };
 
 int pick_cfg(int cout, Cfg* c) {
+    // 32/64-channel layers: 128-position tiles (twice the workgroups of the 256-position ones, half the LDS
+    // per workgroup): r = 512 conv0 451 -> 424 us, r = 1024 bwd conv0 426 -> 396 us, the rest within 1 %
+    // (tools/bench_gemm.py).  SMC_NARROW_BM=256 restores the wide tiles.
+    static const bool narrow128 = !(getenv("SMC_NARROW_BM") && atoi(getenv("SMC_NARROW_BM")) == 256);
     if (cout % 128 == 0) { *c = {128, 128}; return 0; }
-    if (cout % 64 == 0) { *c = {64, 256}; return 1; }
-    if (cout % 32 == 0) { *c = {32, 256}; return 2; }
-    if (cout == 16) { *c = {32, 256}; return 2; }  // half-empty tile, masked
+    if (cout % 64 == 0) {
+        if (narrow128) { *c = {64, 128}; return 5; }
+        *c = {64, 256};
+        return 1;
+    }
+    if (cout % 32 == 0 || cout == 16) {  // cout 16: half-empty tile, masked
+        if (narrow128) { *c = {32, 128}; return 4; }
+        *c = {32, 256};
+        return 2;
+    }
     return -1;
 }
 
@@ -1117,6 +1128,8 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         else if (cfg == 0) SMC_LAUNCH_LDS(2, 2, 2, 2);
         else if (cfg == 1) SMC_LAUNCH_LDS(1, 4, 2, 2);
         else if (cfg == 3) SMC_LAUNCH_LDS(2, 2, 1, 1);
+        else if (cfg == 4) SMC_LAUNCH_LDS(1, 4, 1, 1);
+        else if (cfg == 5) SMC_LAUNCH_LDS(2, 2, 1, 2);
         else SMC_LAUNCH_LDS(1, 4, 1, 2);
 #undef SMC_LAUNCH_LDS
         rc = smc::check_launch("smc_conv_gemm_f32 (LDS-DMA)");
@@ -1140,6 +1153,8 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     } while (0)
     if (cfg == 0) SMC_LAUNCH(2, 2, 2, 2);
     else if (cfg == 1) SMC_LAUNCH(1, 4, 2, 2);
+    else if (cfg == 4) SMC_LAUNCH(1, 4, 1, 1);
+    else if (cfg == 5) SMC_LAUNCH(2, 2, 1, 2);
     else SMC_LAUNCH(1, 4, 1, 2);
 #undef SMC_LAUNCH
     rc = smc::check_launch("smc_conv_gemm_f32");
