@@ -8,8 +8,9 @@
 A step = one find_direction iteration (find_direction.py:292-347) on synthetic inputs that are
 resident in HBM before timing: a config-f FFHQ-1024 generator with seeded weights, S codes
 [129, 26, 512] ~ N(1, 0.5), seeded CLIP ViT-B/32 + IR-SE50, --clip_type small, landmarks 0.
-Each GPU processes a batch of 4 seeds per step (weak scaling: global batch = 4 x N, one RCCL
-all_reduce of the direction gradient per step).  value = images/s = 2 x seeds/s (edited + original
+Each GPU processes a batch of 4 seeds per step (weak scaling: global batch = 4 x N over 129 x N S codes,
+so every GPU runs the single-GPU 129-seed batch schedule; one RCCL all_reduce of the direction gradient
+per step).  value = images/s = 2 x seeds/s (edited + original
 image per seed), seeds counted exactly (the batch picker can draw the short
 last batch of the 129 seeds).
 
@@ -50,7 +51,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--resolution", type=int, default=1024)
     p.add_argument("--batch", type=int, default=4, help="seeds per GPU per step")
-    p.add_argument("--n-seeds", type=int, default=129)
+    p.add_argument("--n-seeds", type=int, default=None,
+                   help="S codes in the run (default 129 per GPU: weak scaling keeps each GPU's batch schedule "
+                        "identical to the single-GPU 129-seed run, short last batch included)")
     p.add_argument("--clip-type", default="small")
     p.add_argument("--clip-impl", default="hip", choices=["hip", "torch"],
                    help="hip: ViT on the gfx950 kernel library (config 4); torch: PyTorch-ROCm ops (config 2)")
@@ -151,7 +154,11 @@ def main():
     from stylemc_amd import synthetic
 
     G = load_generator("synthetic", args.resolution, dev)
-    styles = synthetic.synthetic_styles(args.n_seeds, seed=0).to(dev)
+    # weak scaling: 129 seeds per GPU and a global batch of 4 per GPU give every N the single-GPU schedule
+    # (33 batch indices, the last batch 1 seed per GPU); a fixed 129 seeds at N = 8 would make one draw in
+    # five a 1-seed global batch that leaves 7 of 8 GPUs idle for that step
+    n_seeds = args.n_seeds if args.n_seeds is not None else 129 * world.world_size
+    styles = synthetic.synthetic_styles(n_seeds, seed=0).to(dev)
     clip = build_clip_losses(args.clip_type, dev, "a photo of a face of a feminine woman with no makeup",
                              "a photo of a face of a masculine man", impl=args.clip_impl)
     finder = DirectionFinder(G, styles, clip, IDLoss("a", device=dev, weights=None, impl=args.id_impl), resolution=args.resolution,
@@ -223,6 +230,7 @@ def main():
                                f"IR-SE50 fwd/bwd ({'HIP' if args.id_impl == 'hip' else 'PyTorch-ROCm'}), SGD",
                    "resolution": args.resolution, "batch_per_gpu": args.batch,
                    "global_batch": args.batch * world.world_size, "seeds_per_sec": round(seeds / dt, 3),
+                   "n_seeds": n_seeds, "seeds_per_gpu": n_seeds / world.world_size,
                    "parallelism": f"dp{world.world_size}", "clip_type": args.clip_type, "clip_impl": args.clip_impl, "id_impl": args.id_impl,
                    "batched_loss_pairs": finder.batch_losses, "landmarks_loss_coef": 0,
                    "direction_finite": finite},
