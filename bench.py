@@ -140,7 +140,7 @@ def main():
     from stylemc_amd import _hip, build
     from stylemc_amd import dist as sdist
     world = sdist.init_from_env(use_cuda=True)
-    dev = torch.device("cuda", world.local_rank)
+    dev = torch.device("cuda", world.device_index)
     torch.cuda.set_device(dev)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False

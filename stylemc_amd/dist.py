@@ -13,8 +13,9 @@ import torch.distributed as dist
 
 
 class World:
-    def __init__(self, rank=0, world_size=1, local_rank=0, backend=None):
+    def __init__(self, rank=0, world_size=1, local_rank=0, backend=None, device_index=None):
         self.rank, self.world_size, self.local_rank, self.backend = rank, world_size, local_rank, backend
+        self.device_index = local_rank if device_index is None else device_index
 
     @property
     def distributed(self):
@@ -23,7 +24,7 @@ class World:
     def barrier(self):
         if self.distributed:
             if self.backend == "nccl":
-                dist.barrier(device_ids=[self.local_rank])
+                dist.barrier(device_ids=[self.device_index])
             else:
                 dist.barrier()
 
@@ -47,14 +48,17 @@ def init_from_env(use_cuda=True):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size <= 1:
         return World()
-    backend = "nccl" if use_cuda else "gloo"
+    # rehearsal knobs for a one-GPU box: SMC_DIST_BACKEND=gloo (RCCL refuses two ranks on one GPU) and
+    # SMC_SHARE_GPU=1 (every rank on device 0); the production path is RCCL with one GPU per rank
+    backend = os.environ.get("SMC_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
+    device_index = 0 if os.environ.get("SMC_SHARE_GPU") == "1" else local_rank
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if use_cuda:
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(device_index)
     if not dist.is_initialized():
-        kw = {"device_id": torch.device("cuda", local_rank)} if use_cuda else {}
+        kw = {"device_id": torch.device("cuda", device_index)} if use_cuda and backend == "nccl" else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world_size, **kw)
-    return World(rank, world_size, local_rank, backend)
+    return World(rank, world_size, local_rank, backend, device_index)
 
 
 def shard_rows(lo, hi, rank, world_size):

@@ -344,7 +344,7 @@ def _cli():
                        init_std):
         from .id_loss import IDLoss
         world = _dist.init_from_env(use_cuda=True)
-        device = torch.device("cuda", world.local_rank)
+        device = torch.device("cuda", world.device_index)
         torch.cuda.set_device(device)
         if landmarks_loss_coef != 0:
             warnings.warn("landmarks loss adds no gradient in the reference (no_grad, find_direction.py:90); ignored")
