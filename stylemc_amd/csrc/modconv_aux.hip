@@ -310,12 +310,12 @@ __global__ __launch_bounds__(256) void blur_act_fast(const float* t, int nsplit,
 // Backward of conv0's epilogue + FIR in one pass: du = act'(g; y(u)) * d (re-derived per element of the
 // haloed tile), dT = FIR^T(du) (pad (pady0, padx0) of the adjoint), dd[n,o] += sum dz*u over the du
 // positions this tile owns (its own 32x64 window, so every position is counted exactly once).
-template <int FH, int FW>
+template <int FH, int FW, bool V2 = false>
 __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const float* u, float* dt, float* dd, int c,
                                                          int u_h, int u_w, int t_h, int t_w, const float* f, int padx0,
                                                          int pady0, float fgain, int flip, Epi e) {
     constexpr int ROWS = kFH + FH - 1, COLS = kFW + FW - 1, STRIDE = COLS + 1;
-    __shared__ float tile[ROWS * STRIDE];
+    __shared__ __attribute__((aligned(16))) float tile[ROWS * STRIDE];
     __shared__ float red[4];
     const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
     const int ox0 = blockIdx.x * kFW, oy0 = blockIdx.y * kFH;
@@ -330,36 +330,67 @@ __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const f
     const int64_t uplane = nc * (int64_t)u_h * u_w;
     float part = 0.f;
     // fixed-trip unrolled loads (u, g, noise of every element in flight at once), then the math
-    constexpr int NL = (ROWS * COLS + 255) / 256;
-    float uv[NL], gv[NL], nv[NL];
     const float* up = u + uplane;
     const float* gp = g + uplane;
     const float* np_ = e.noise ? e.noise + n * e.noise_nstride : nullptr;
+    auto elem = [&](float uu, float gg, float nn, int iy, int ix) {
+        const float yv = smc::epi_y(uu, dv, nn * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
+        const float dz = smc::act_grad_y(e.act, gg, yv, e.alpha, e.gain, e.clamp);
+        if (iy >= oy0 && iy < oy0 + kFH && ix >= ox0 && ix < ox0 + kFW) part += dz * uu;
+        return dz * dv;
+    };
+    if constexpr (V2) {
+        // u_w and padx0 even: the tile row splits into aligned column pairs that are in or out together
+        constexpr int C2 = (COLS + 1) / 2;  // pairs per row (the last pair's second column is the pad column)
+        constexpr int NL = (ROWS * C2 + 255) / 256;
+        float2 uv[NL], gv[NL], nv[NL];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) {
-        const int i = tid + 256 * l;
-        const int r = i / COLS, cc = i - r * COLS;
-        const int iy = iy0 + r, ix = ix0 + cc;
-        const bool ok = i < ROWS * COLS && iy >= 0 && iy < u_h && ix >= 0 && ix < u_w;
-        const int pix = ok ? iy * u_w + ix : 0;
-        uv[l] = up[pix];
-        gv[l] = gp[pix];
-        nv[l] = np_ ? np_[pix] : 0.f;
-    }
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-        const int i = tid + 256 * l;
-        const int r = i / COLS, cc = i - r * COLS;
-        const int iy = iy0 + r, ix = ix0 + cc;
-        const bool ok = i < ROWS * COLS && iy >= 0 && iy < u_h && ix >= 0 && ix < u_w;
-        float v = 0.f;
-        if (ok) {
-            const float yv = smc::epi_y(uv[l], dv, nv[l] * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
-            const float dz = smc::act_grad_y(e.act, gv[l], yv, e.alpha, e.gain, e.clamp);
-            v = dz * dv;
-            if (iy >= oy0 && iy < oy0 + kFH && ix >= ox0 && ix < ox0 + kFW) part += dz * uv[l];
+        for (int l = 0; l < NL; ++l) {
+            const int i = tid + 256 * l;
+            const int r = i / C2, c2 = i - r * C2;
+            const int iy = iy0 + r, ix = ix0 + 2 * c2;
+            const bool ok = i < ROWS * C2 && iy >= 0 && iy < u_h && ix >= 0 && ix < u_w;
+            const int pix = ok ? iy * u_w + ix : 0;
+            uv[l] = *reinterpret_cast<const float2*>(up + pix);
+            gv[l] = *reinterpret_cast<const float2*>(gp + pix);
+            nv[l] = np_ ? *reinterpret_cast<const float2*>(np_ + pix) : make_float2(0.f, 0.f);
         }
-        if (i < ROWS * COLS) tile[r * STRIDE + cc] = v;
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            const int i = tid + 256 * l;
+            const int r = i / C2, c2 = i - r * C2;
+            const int iy = iy0 + r, ix = ix0 + 2 * c2;
+            const bool ok = i < ROWS * C2 && iy >= 0 && iy < u_h && ix >= 0 && ix < u_w;
+            float2 v = make_float2(0.f, 0.f);
+            if (ok) {
+                v.x = elem(uv[l].x, gv[l].x, nv[l].x, iy, ix);
+                v.y = elem(uv[l].y, gv[l].y, nv[l].y, iy, ix + 1);
+            }
+            if (i < ROWS * C2) *reinterpret_cast<float2*>(&tile[r * STRIDE + 2 * c2]) = v;
+        }
+    } else {
+        constexpr int NL = (ROWS * COLS + 255) / 256;
+        float uv[NL], gv[NL], nv[NL];
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            const int i = tid + 256 * l;
+            const int r = i / COLS, cc = i - r * COLS;
+            const int iy = iy0 + r, ix = ix0 + cc;
+            const bool ok = i < ROWS * COLS && iy >= 0 && iy < u_h && ix >= 0 && ix < u_w;
+            const int pix = ok ? iy * u_w + ix : 0;
+            uv[l] = up[pix];
+            gv[l] = gp[pix];
+            nv[l] = np_ ? np_[pix] : 0.f;
+        }
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            const int i = tid + 256 * l;
+            const int r = i / COLS, cc = i - r * COLS;
+            const int iy = iy0 + r, ix = ix0 + cc;
+            const bool ok = i < ROWS * COLS && iy >= 0 && iy < u_h && ix >= 0 && ix < u_w;
+            const float v = ok ? elem(uv[l], gv[l], nv[l], iy, ix) : 0.f;
+            if (i < ROWS * COLS) tile[r * STRIDE + cc] = v;
+        }
     }
     __syncthreads();
     float out[4][2];
@@ -628,7 +659,13 @@ SMC_API int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* 
         return SMC_ERR_UNSUPPORTED;
     }
     dim3 grid((unsigned)smc::ceil_div(t_w, kFW), (unsigned)smc::ceil_div(t_h, kFH), (unsigned)(n * c));
-    hipLaunchKernelGGL((blur_act_bwd_fast<4, 4>), grid, dim3(256), 0, smc::as_stream(stream), g, u, dt, dd, c, u_h, u_w,
-                       t_h, t_w, f, padx0, pady0, fgain, flip, to_epi(epi));
+    const bool v2 = u_w % 2 == 0 && padx0 % 2 == 0 && epi->noise_nstride % 2 == 0 &&
+                    (((uintptr_t)g | (uintptr_t)u | (uintptr_t)epi->noise) & 7) == 0;
+    if (v2)
+        hipLaunchKernelGGL((blur_act_bwd_fast<4, 4, true>), grid, dim3(256), 0, smc::as_stream(stream), g, u, dt, dd, c,
+                           u_h, u_w, t_h, t_w, f, padx0, pady0, fgain, flip, to_epi(epi));
+    else
+        hipLaunchKernelGGL((blur_act_bwd_fast<4, 4>), grid, dim3(256), 0, smc::as_stream(stream), g, u, dt, dd, c, u_h,
+                           u_w, t_h, t_w, f, padx0, pady0, fgain, flip, to_epi(epi));
     return smc::check_launch("smc_modconv_blur_act_bwd_f32");
 }
