@@ -173,6 +173,15 @@ int smc_torgb_fwd_f32(const float* x, const float* w, const float* s, const floa
 int smc_torgb_bwd_f32(const float* g, const float* y, const float* w, const float* s, float* dx, int n, int cin,
                       int cout, int h, int w_, float clamp, int scale, int accumulate, void* stream);
 
+/* IDLoss face crop (id_loss.py:20-23): y[p] = adaptive_avg_pool(crop(adaptive_avg_pool(x[p], (pool_h, pool_w)),
+ * [crop_y0 : crop_y0+crop_h, crop_x0 : crop_x0+crop_w]), (out_h, out_w)) for `planes` planes; the first pool
+ * must be an integer factor (in = pool * k, else SMC_ERR_UNSUPPORTED).  The backward writes the whole input
+ * gradient dx [planes][in_h][in_w] (zeros outside the crop). */
+int smc_face_crop_f32(const float* x, int64_t planes, int in_h, int in_w, int pool_h, int pool_w, int crop_y0,
+                      int crop_x0, int crop_h, int crop_w, int out_h, int out_w, float* y, void* stream);
+int smc_face_crop_bwd_f32(const float* dy, int64_t planes, int in_h, int in_w, int pool_h, int pool_w, int crop_y0,
+                          int crop_x0, int crop_h, int crop_w, int out_h, int out_w, float* dx, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * CLIP ViT image tower (replaces the third-party openai/CLIP VisionTransformer that the reference
  * calls through CLIPLoss.encode_image, clip_loss.py:21,25-26; weights frozen -> data gradient only).

@@ -14,6 +14,35 @@ from torch import nn
 from .model_irse import build_irse50
 
 
+# id_loss.py:20-23 geometry: pool to 256, crop [35:223, 32:220] (188 x 188), pool to 112
+_POOL, _CROP, _OUT = 256, (35, 32, 188, 188), 112
+
+
+class FaceCropFn(torch.autograd.Function):
+    """The face crop as one gfx950 kernel each way (smc_face_crop_f32 / _bwd_f32)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        from .. import _hip
+        x = x.contiguous()
+        n, c, h, w = x.shape
+        y = torch.empty(n, c, _OUT, _OUT, device=x.device, dtype=torch.float32)
+        _hip.call("smc_face_crop_f32", _hip.ptr(x), n * c, h, w, _POOL, _POOL, *_CROP, _OUT, _OUT, y.data_ptr(),
+                  _hip.stream())
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .. import _hip
+        gy = gy.contiguous()
+        n, c, h, w = ctx.shape
+        dx = torch.empty(ctx.shape, device=gy.device, dtype=torch.float32)
+        _hip.call("smc_face_crop_bwd_f32", _hip.ptr(gy), n * c, h, w, _POOL, _POOL, *_CROP, _OUT, _OUT, dx.data_ptr(),
+                  _hip.stream())
+        return dx
+
+
 class IDLoss(nn.Module):
     def __init__(self, opts=None, facenet=None, weights="id_loss/model_ir_se50.pth", device="cuda", seed=3,
                  impl="hip"):
@@ -31,10 +60,14 @@ class IDLoss(nn.Module):
                 raise ValueError(f"impl must be 'hip' or 'torch', got {impl!r}")
         self.facenet = facenet.eval()
         self.opts = opts
+        self.fused_crop = impl == "hip"
 
-    @staticmethod
-    def face_crop(x):
-        """id_loss.py:20-23: pool to 256, crop [35:223, 32:220], pool to 112."""
+    def face_crop(self, x):
+        """id_loss.py:20-23: pool to 256, crop [35:223, 32:220], pool to 112 (one HIP kernel each way on the
+        hip path when the input is an integer multiple of 256 px; the PyTorch ops otherwise)."""
+        if (self.fused_crop and x.is_cuda and x.dtype == torch.float32 and x.shape[2] % _POOL == 0
+                and x.shape[3] % _POOL == 0 and x.shape[3] // _POOL in (1, 2, 4)):
+            return FaceCropFn.apply(x)
         if x.shape[2] != 256:
             x = F.adaptive_avg_pool2d(x, (256, 256))
         x = x[:, :, 35:223, 32:220]
