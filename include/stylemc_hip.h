@@ -182,6 +182,15 @@ int smc_face_crop_f32(const float* x, int64_t planes, int in_h, int in_w, int po
 int smc_face_crop_bwd_f32(const float* dy, int64_t planes, int in_h, int in_w, int pool_h, int pool_w, int crop_y0,
                           int crop_x0, int crop_h, int crop_w, int out_h, int out_w, float* dx, void* stream);
 
+/* CLIP input preprocessing (find_direction.py:49-52): y = (bicubic(clamp(img*127.5+128, 0, 255), out) / 255
+ * - mean[c]) / std[c], bicubic = F.interpolate(mode='bicubic', align_corners=False) (A = -0.75).  img
+ * [n][channels][in_h][in_w] -> y [n][channels][out_h][out_w]; mean/std: `channels` floats on the device.
+ * The backward writes the whole image gradient dimg (downsampling, in >= out, only). */
+int smc_clip_unprocess_f32(const float* img, int n, int channels, int in_h, int in_w, int out_h, int out_w,
+                           const float* mean, const float* std_, float* y, void* stream);
+int smc_clip_unprocess_bwd_f32(const float* img, const float* dy, int n, int channels, int in_h, int in_w, int out_h,
+                               int out_w, const float* mean, const float* std_, float* dimg, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * CLIP ViT image tower (replaces the third-party openai/CLIP VisionTransformer that the reference
  * calls through CLIPLoss.encode_image, clip_loss.py:21,25-26; weights frozen -> data gradient only).

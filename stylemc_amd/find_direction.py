@@ -37,8 +37,41 @@ S_NON_TRAINABLE_SPACE_CHANNELS = utils.S_NON_TRAINABLE_SPACE_CHANNELS
 RESOLUTION_DICT = {256: 6, 512: 7, 1024: 8}
 
 
+class UnprocessFn(torch.autograd.Function):
+    """unprocess() for square fp32 GPU images downsampled to `size`: one gfx950 kernel each way
+    (smc_clip_unprocess_f32 / _bwd_f32, csrc/unprocess.hip)."""
+
+    @staticmethod
+    def forward(ctx, img, mean, std, size):
+        from . import _hip
+        img = img.contiguous()
+        n, c, h, w = img.shape
+        mean = mean.reshape(-1).contiguous()
+        std = std.reshape(-1).contiguous()
+        y = torch.empty(n, c, size, size, device=img.device, dtype=torch.float32)
+        _hip.call("smc_clip_unprocess_f32", _hip.ptr(img), n, c, h, w, size, size, _hip.ptr(mean), _hip.ptr(std),
+                  y.data_ptr(), _hip.stream())
+        ctx.save_for_backward(img, mean, std)
+        ctx.size = size
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import _hip
+        img, mean, std = ctx.saved_tensors
+        n, c, h, w = img.shape
+        gy = gy.contiguous()
+        dimg = torch.empty_like(img)
+        _hip.call("smc_clip_unprocess_bwd_f32", _hip.ptr(img), _hip.ptr(gy), n, c, h, w, ctx.size, ctx.size,
+                  _hip.ptr(mean), _hip.ptr(std), dimg.data_ptr(), _hip.stream())
+        return dimg, None, None, None
+
+
 def unprocess(img, mean, std, size=224):
     """find_direction.py:49-52 with torchvision-0.8 tensor Resize(224, BICUBIC) + CenterCrop(224)."""
+    if (img.is_cuda and img.dtype == torch.float32 and img.ndim == 4 and img.shape[2] == img.shape[3]
+            and img.shape[2] >= size and mean.numel() == img.shape[1]):
+        return UnprocessFn.apply(img, mean, std, size)
     x = (img * 127.5 + 128).clamp(0, 255)
     h, w = x.shape[-2:]
     nh, nw = (size, int(size * w / h)) if h <= w else (int(size * h / w), size)

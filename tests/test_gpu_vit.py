@@ -270,3 +270,27 @@ def test_clip_pair_loss_equals_separate_encodes():
     (g2,) = torch.autograd.grad(l2.sum(), t2)
     close(l2, l1, 1e-5, "pair vs separate loss")
     close(g2, g1, 1e-4, "pair vs separate gradient")
+
+
+@pytest.mark.parametrize("res", [1024, 512, 256, 224])
+def test_unprocess_kernel_vs_torch_ops(res):
+    """UnprocessFn (smc_clip_unprocess_f32/_bwd_f32) == (img*127.5+128).clamp(0,255) -> F.interpolate bicubic
+    (align_corners=False) -> (x/255 - mean)/std (find_direction.py:49-52) on the same GPU tensors; inputs
+    scaled so that the clamp is active on part of the image."""
+    import torch.nn.functional as F
+    from stylemc_amd import utils
+    from stylemc_amd.find_direction import UnprocessFn
+    mean, std = utils.get_mean_std(DEV)
+    g = torch.Generator().manual_seed(res)
+    img = (1.3 * torch.randn(2, 3, res, res, generator=g)).to(DEV)
+    cot = torch.randn(2, 3, 224, 224, generator=g).to(DEV)
+    a = img.clone().requires_grad_(True)
+    ya = UnprocessFn.apply(a, mean, std, 224)
+    (da,) = torch.autograd.grad(ya, a, cot)
+    b = img.clone().requires_grad_(True)
+    x = (b * 127.5 + 128).clamp(0, 255)
+    x = F.interpolate(x, size=(224, 224), mode="bicubic", align_corners=False)
+    yb = (x / 255 - mean) / std
+    (db,) = torch.autograd.grad(yb, b, cot)
+    close(ya, yb, 1e-5, "unprocess")
+    close(da, db, 1e-5, "unprocess gradient")
