@@ -488,6 +488,145 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_lds_kernel(GemmParams p) {
     gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32);
 }
 
+// Halo-tile variant for the 32-output-channel 3x3 stride-1 'same' convs (the r = 1024 conv1, forward and data
+// gradient).  With only 32 output channels the tap-major GEMM above re-reads every input pixel once per tap
+// (9x) through L2 for 16 FLOP per LDS byte.  Here a workgroup owns one row segment of BM positions and stages,
+// per CK-channel step, the 3-row halo X[CK][3][BM+2] plus all taps' weight slabs W[9][CK][32]; the nine taps
+// then run out of LDS (27-35 FLOP per staged byte).  Persistent: workgroup g takes tiles g, g + G, ...; the
+// (tile, channel-step) sequence is one 2-stage LDS ring, so the next tile's halo lands during this tile's
+// MFMAs and epilogue.  With G a multiple of 8 a column segment stays on one XCD (tile % 8 == XCD), and the
+// rows that share halo lines run concurrently on the same L2.
+template <int TM, int CK>
+__global__ __launch_bounds__(NT, 2) void conv3_halo_kernel(GemmParams p, int ntiles) {
+    constexpr int BO = 32;
+    constexpr int BM = 4 * TM * 32;                 // positions of one row segment (4 waves x TM blocks)
+    constexpr int HWD = BM + 2;                     // halo row width
+    // floats per channel of the halo, padded to 32 mod 64 so the two half-waves' B reads (channels k, k+1)
+    // fall on disjoint LDS banks
+    constexpr int CH = ((3 * HWD - 32 + 63) / 64) * 64 + 32;
+    constexpr int XF = CK * CH;
+    constexpr int XCH = (XF + 63) / 64;             // 64-float DMA chunks of the halo
+    constexpr int XS = XCH * 64;
+    constexpr int WT = CK * BO;                     // one tap's weight slab
+    static_assert(WT == 256 || WT == 128, "16-B-per-lane weight DMAs cover one or two tap slabs");
+    constexpr int TPD = 256 / WT;                   // tap slabs per weight DMA
+    constexpr int ND = (9 + TPD - 1) / TPD;         // weight DMAs per step
+    constexpr int STAGE = XS + ND * 256;
+    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave;
+    const PhaseDev& ph = p.ph[0];
+    const int H = p.in_h, W = p.in_w;
+    const int hw = H * W;
+    const int tpr = W / BM;                         // tiles per row
+    const int kpt = p.cin / CK;                     // channel steps per tile
+    const int G = gridDim.x;
+    const int nmine = (int)blockIdx.x < ntiles ? (ntiles - (int)blockIdx.x + G - 1) / G : 0;
+    const int S = nmine * kpt;
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * hw * 4), 0x00020000);
+    int toff[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) toff[t] = (ph.dy[t] + 1) * HWD + (ph.dx[t] + 1);
+
+    auto decode = [&](int ti, int& n, int& a, int& b0) {
+        int t = (int)blockIdx.x + ti * G;
+        const int bs = t % tpr;
+        t /= tpr;
+        a = t % H;
+        n = t / H;
+        b0 = bs * BM;
+    };
+    auto issue = [&](int s) {
+        const int ti = s / kpt;
+        const int ci0 = (s - ti * kpt) * CK;
+        int n, a, b0;
+        decode(ti, n, a, b0);
+        float* xs = smem + (s & 1) * STAGE;
+        const int cbase = n * p.cin + ci0;
+        // halo chunk -> per-lane source offset; branch-free (out-of-range lanes read 0 via the buffer bound)
+        auto halo_dma = [&](int chunk) {
+            const int f = chunk * 64 + lane;
+            const int ch = f / CH;
+            const int rem = f - ch * CH;
+            const int r = rem / HWD;
+            const int c = rem - r * HWD;
+            const int iy = a + r - 1, ix = b0 + c - 1;
+            const bool ok = f < XF && r < 3 && iy >= 0 && iy < H && ix >= 0 && ix < W;
+            const int v = (((cbase + ch) * H + iy) * W + ix) * 4;
+            const int msk = -(int)ok;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (__attribute__((address_space(3))) void*)(xs + chunk * 64),
+                                                     4, (v & msk) | (0x7ffffff0 & ~msk), 0, 0, 0);
+        };
+#pragma unroll
+        for (int j = 0; j < XCH / 4; ++j) halo_dma(wave + 4 * j);
+        if (wave < XCH % 4) halo_dma(4 * (XCH / 4) + wave);
+        const float* wb = ph.wk + (ph.wstride ? (int64_t)n * ph.wstride : 0) + (int64_t)ci0 * BO +
+                          (lane % (64 / TPD)) * 4;
+        auto w_dma = [&](int d) {
+            const int t = std::min(d * TPD + lane / (64 / TPD), 8);  // a tenth slab (TPD 2) re-reads tap 8 into padding
+            __builtin_amdgcn_global_load_lds((const void*)(wb + (int64_t)t * p.cin * BO),
+                                             (__attribute__((address_space(3))) void*)(xs + XS + d * 256), 16, 0, 0);
+        };
+#pragma unroll
+        for (int j = 0; j < ND / 4; ++j) w_dma(wave + 4 * j);
+        if (wave < ND % 4) w_dma(4 * (ND / 4) + wave);
+    };
+
+    f32x16 acc[1][TM];
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.f;
+    const int kh = lane >> 5, l32 = lane & 31;
+    if (S > 0) issue(0);
+    for (int s = 0; s < S; ++s) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // step s landed for every wave; slot (s+1)&1 is no longer read
+        asm volatile("" ::: "memory");
+        const float* Xs = smem + (s & 1) * STAGE + kh * CH + wm * TM * 32 + l32;
+        const float* Ws = smem + (s & 1) * STAGE + XS + kh * BO + l32;
+        // fragments of tap t+1 are read under tap t's MFMAs; the next step's DMAs go out after tap 0's
+        float af[2][CK / 2], bf[2][CK / 2][TM];
+        auto frag = [&](int t, int b) {
+#pragma unroll
+            for (int q = 0; q < CK / 2; ++q) {
+                af[b][q] = Ws[t * WT + 2 * q * BO];
+#pragma unroll
+                for (int j = 0; j < TM; ++j) bf[b][q][j] = Xs[toff[t] + 2 * q * CH + j * 32];
+            }
+        };
+        frag(0, 0);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            if (t + 1 < 9) frag(t + 1, (t + 1) & 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < CK / 2; ++q)
+#pragma unroll
+                for (int j = 0; j < TM; ++j)
+                    acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t & 1][q], bf[t & 1][q][j], acc[0][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (t == 0 && s + 1 < S) issue(s + 1);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int ti = s / kpt;
+        if (s - ti * kpt == kpt - 1) {
+            int n, a, b0;
+            decode(ti, n, a, b0);
+            const int m0 = n * hw + a * W + b0;
+            gemm_epilogue<1, 4, 1, TM>(p, ph, acc, m0, 0, p.n * hw, hw, 0, 0, wm, kh, l32);
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.f;
+        }
+    }
+}
+
 // Style-scaled input for the low-resolution layers: out[n][i][p] = x[n][i][p] * s[n][i] (float4 when hw % 4 == 0).
 __global__ __launch_bounds__(256) void xscale_kernel(const float* x, const float* s, float* out, int64_t hw,
                                                      int64_t planes) {
@@ -850,6 +989,22 @@ bool lds_shape_ok(int n, int cin, int cout, int in_h, int in_w, const smc_conv_p
     return !off && cout % c.bo == 0 && cin % BK == 0 && (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31);
 }
 
+// conv3_halo_kernel<1, 8> shapes: one 9-tap phase with |dy|, |dx| <= 1 that maps the input grid onto an
+// equal output grid (3x3 stride-1 'same'), 32 output channels, cin % 8 == 0, rows of whole 128-position
+// segments.  Opt-in (SMC_HALO=1): measured slower than the tap-major LDS-DMA kernel on the r = 1024 conv1
+// (962 vs 822 us), kept as the A/B baseline for the next attempt.
+bool halo_ok(int n, int cin, int cout, int in_h, int in_w, int y_h, int y_w, const smc_conv_phase* ph, int nph) {
+    static const bool on = getenv("SMC_HALO") && atoi(getenv("SMC_HALO")) != 0;
+    if (!on || nph != 1 || cout != 32 || cin % 8 != 0 || in_w % 128 != 0) return false;
+    const smc_conv_phase& q = ph[0];
+    if (q.ntaps != 9 || q.in_stride != 1 || q.out_h != in_h || q.out_w != in_w || y_h != in_h || y_w != in_w ||
+        q.out_oy != 0 || q.out_ox != 0 || q.out_sy != 1 || q.out_sx != 1)
+        return false;
+    for (int t = 0; t < 9; ++t)
+        if (q.tap_dy[t] < -1 || q.tap_dy[t] > 1 || q.tap_dx[t] < -1 || q.tap_dx[t] > 1) return false;
+    return (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31);
+}
+
 // floats of per-sample weights (n x sum_p taps_p * cin * cout), 64-float aligned
 int64_t wsample_floats(int n, int cin, int cout, const smc_conv_phase* ph, int nph) {
     int64_t t = 0;
@@ -1108,6 +1263,23 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             if (rc != SMC_OK) return rc;
         }
         p.s = nullptr;
+        if (nsplit == 1 && halo_ok(n, cin, cout, in_h, in_w, y_h, y_w, phases, nphases)) {
+            static const int wpc = [] {
+                const char* f = getenv("SMC_HALO_WPC");
+                return f && atoi(f) > 0 ? atoi(f) : 3;
+            }();
+            static const int tm = getenv("SMC_HALO_TM") && atoi(getenv("SMC_HALO_TM")) == 2 ? 2 : 1;  // A/B knobs
+            static const int ck = getenv("SMC_HALO_CK") && atoi(getenv("SMC_HALO_CK")) == 4 ? 4 : 8;
+            const int bm = tm == 2 && in_w % 256 == 0 ? 256 : 128;
+            const int ntiles = n * in_h * (in_w / bm);
+            const int g = std::min(ntiles, smc::device_cu_count() * (bm == 256 ? 2 : wpc));
+            if (bm == 256) hipLaunchKernelGGL((conv3_halo_kernel<2, 8>), dim3((unsigned)g), dim3(NT), 0, st, p, ntiles);
+            else if (ck == 4)
+                hipLaunchKernelGGL((conv3_halo_kernel<1, 4>), dim3((unsigned)std::min(ntiles, smc::device_cu_count() * 4)),
+                                   dim3(NT), 0, st, p, ntiles);
+            else hipLaunchKernelGGL((conv3_halo_kernel<1, 8>), dim3((unsigned)g), dim3(NT), 0, st, p, ntiles);
+            return smc::check_launch("smc_conv_gemm_f32 (halo tile)");
+        }
         static const bool no_swz = getenv("SMC_NO_XCD_SWIZZLE") != nullptr;  // A/B knob
         if (!no_swz) {
             p.ntn = (int)grid.y;

@@ -197,6 +197,32 @@ def test_synthesis_layer_grad_subsets():
     close(dxc, dxa, 1e-6, "dx only")
 
 
+@pytest.mark.parametrize("n,cin,r", [(2, 32, 256), (4, 64, 128), (1, 32, 1024)])
+def test_conv_gemm_32ch_vs_conv2d(n, cin, r):
+    """The 32-output-channel 3x3 'same' convs (the r = 1024 conv1 class): forward (per-sample style-scaled
+    weights) and the data gradient (shared flipped weights) against an fp64 CPU convolution (no activation,
+    so no kinks: tolerance 2e-5 of the max).  Under SMC_HALO=1 (tools/halo_ab.sh) the same shapes run
+    conv3_halo_kernel."""
+    import torch.nn.functional as F
+    from stylemc_amd import _hip, modconv
+    gen = torch.Generator().manual_seed(11)
+    W = torch.randn(32, cin, 3, 3, generator=gen)
+    P = modconv.PackedConv(W.to(DEV), 1)
+    x = torch.randn(n, cin, r, r, generator=gen)
+    s = torch.randn(n, cin, generator=gen) * 0.5 + 1
+    ph, nph, _, _ = P.fwd_phases(r, r)
+    y = torch.empty(n, 32, r, r, device=DEV)
+    modconv.gemm(x.to(DEV), y, ph, nph, cin, 32, s=s.to(DEV), epi=modconv._epilogue(_hip.EPI_STORE))
+    ref = F.conv2d((x * s[:, :, None, None]).double(), W.double(), padding=1)
+    close(y, ref, 2e-5, "halo fwd")
+    g = torch.randn(n, 32, r, r, generator=gen)
+    phb, nphb = P.bwd_phases(r, r)
+    dx = torch.empty(n, cin, r, r, device=DEV)
+    modconv.gemm(g.to(DEV), dx, phb, nphb, 32, cin, epi=modconv._epilogue(_hip.EPI_STORE))
+    refb = F.conv_transpose2d(g.double(), W.double(), padding=1)
+    close(dx, refb, 2e-5, "halo data grad")
+
+
 @pytest.mark.parametrize("cin,res,n,clamp", [(512, 4, 2, 256.0), (64, 64, 3, 0.3), (32, 128, 1, None), (128, 9, 2, 1.0)])
 def test_torgb_vs_oracle(cin, res, n, clamp):
     o, p = _pair_layers(cin, 3, res, 1, clamp=clamp, kind="rgb")
