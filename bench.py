@@ -24,10 +24,12 @@ taken by the other stream's kernels), against the fp32 MFMA peak (157.3 TFLOP/s,
 MI355X_MICROARCH.md).  traffic: HBM bytes per launch from the rocprofv3 PMC pass recorded in
 profiles/pmc_traffic.json (null if absent).
 
-cpu_baseline (rank 0, N=1): the test oracle (pure-torch fp32 CPU restatement of the reference
-algorithm, oracle/) running the same step at FFHQ-1024 with batch 1 for --cpu-iters iterations on
---cpu-threads host threads.  parity (same run): the GPU path repeats that exact oracle run and reports
-the cosine similarity of the two final directions (the metric's "dir cosine-sim vs ref").
+cpu_baseline (rank 0, N=1): the test oracle (pure-torch fp32 CPU restatement of the reference loop,
+oracle/, pinned to the reference by tests/golden) running the same step at FFHQ-1024, batch 4: 1 warm-up +
+3 timed iterations on the host's CPU share (affinity set capped by the cgroup quota; os.cpu_count() and the
+CPU model are reported beside it).  parity (same run): the GPU path repeats that exact oracle run and
+reports the cosine similarity of the two final directions (the metric's "dir cosine-sim vs ref").  N > 1:
+parity = the N-rank direction vs rank 0 re-running the same global batch in one process.
 """
 import argparse
 import json
@@ -59,8 +61,9 @@ def parse():
                    help="hip: ViT on the gfx950 kernel library (config 4); torch: PyTorch-ROCm ops (config 2)")
     p.add_argument("--id-impl", default="hip", choices=["hip", "torch"],
                    help="hip: IR-SE50 on the gfx950 kernel library (config 4); torch: PyTorch-ROCm/MIOpen (config 2)")
-    p.add_argument("--cpu-iters", type=int, default=4)
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-iters", type=int, default=4, help="CPU baseline / parity iterations (first = warm-up)")
+    p.add_argument("--cpu-batch", type=int, default=4)
+    p.add_argument("--cpu-threads", type=int, default=0, help="0: the host's CPU share (affinity, cgroup quota)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timer", action="store_true", help="skip the roofline pass")
     p.add_argument("--roofline-steps", type=int, default=2, help="serialised steps timed per launch for the roofline")
@@ -69,59 +72,141 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(resolution, iters, threads):
-    """Oracle find_direction on the host: `iters` iterations, batch 1 (TEST ORACLE used as the baseline)."""
-    from oracle import find_direction as OF
+def host_cpus():
+    """Threads the CPU baseline may use on this host, and how that was decided: the scheduler affinity set,
+    capped by the cgroup CPU quota (a GPU box shares a large machine; os.cpu_count() reports all of it)."""
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    info["affinity"] = aff
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    info["cgroup_quota_cpus"] = quota
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    info["model"] = model
+    threads = min(aff, quota) if quota else aff
+    return max(1, threads), info
+
+
+def _oracle_problem(resolution):
     from oracle import losses as OL
     from oracle import networks as ON
     from oracle import synthesis as OS
     from stylemc_amd import synthetic
-    from stylemc_amd.find_direction import initial_delta
-    torch.set_num_threads(threads)
     cfg = synthetic.generator_config(resolution=resolution)
     sd = synthetic.generator_state_dict(cfg, seed=0)
     G = torch.nn.Module()
     G.synthesis = ON.SynthesisNetwork(512, resolution, 3, channel_base=cfg["channel_base"], conv_clamp=256.0)
     G.synthesis.load_state_dict({k[10:]: v for k, v in sd.items() if k.startswith("synthesis.")}, strict=False)
     G.eval().requires_grad_(False)
-    shapes = OS.get_temp_shapes(G)
     vis = OL.CLIPVisual().eval()
     vis.load_state_dict(synthetic.seeded_state_dict(vis, seed=4))
     vis.requires_grad_(False)
-    clip = OL.CLIPLoss(vis, synthetic.text_direction("a photo of a face of a feminine woman with no makeup",
-                                                     "a photo of a face of a masculine man"))
+    clip = OL.CLIPLoss(vis, synthetic.text_direction(*TEXT))
     net = OL.IRSE50().eval()
     net.load_state_dict(synthetic.seeded_state_dict(net, seed=3))
     net.requires_grad_(False)
-    styles = synthetic.synthetic_styles(iters, seed=0)
+    return G, OS.get_temp_shapes(G), clip, OL.IDLoss(net)
+
+
+# the CPU baseline / parity problem: PARITY_ITEMS S codes, batch 4, PARITY_ITERS iterations (the first is
+# the CPU baseline's warm-up), 2 epochs so the cosine schedule covers them
+PARITY_ITEMS, PARITY_EPOCHS = 8, 2
+TEXT = ("a photo of a face of a feminine woman with no makeup", "a photo of a face of a masculine man")
+
+
+def cpu_baseline(resolution, batch, iters, threads, cpu_info):
+    """Oracle find_direction on the host (TEST ORACLE used as the baseline): `iters` iterations at `batch`,
+    the first one untimed (warm-up)."""
+    from oracle import find_direction as OF
+    from stylemc_amd import synthetic
+    from stylemc_amd.find_direction import initial_delta
+    torch.set_num_threads(threads)
+    G, shapes, clip, idl = _oracle_problem(resolution)
+    styles = synthetic.synthetic_styles(PARITY_ITEMS, seed=0)
+    log = []
     t0 = time.perf_counter()
-    _, delta = OF.find_direction(G, styles, clip, OL.IDLoss(net), shapes, int(resolution).bit_length() - 3,
-                                 batch_size=1, n_epochs=1, max_iterations=iters, init_delta=initial_delta(0, 0.01))
-    dt = time.perf_counter() - t0
-    return {"value": 2 * iters / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{iters} find_direction iterations x 1 seed (FFHQ-{resolution}, CLIP ViT-B/32 + IR-SE50) "
-                      f"in {dt:.1f} s, oracle/ pure-torch fp32 CPU restatement, {threads} threads"}, delta.detach()
+    _, delta = OF.find_direction(G, styles, clip, idl, shapes, int(resolution).bit_length() - 3, batch_size=batch,
+                                 n_epochs=PARITY_EPOCHS, max_iterations=iters, init_delta=initial_delta(0, 0.01),
+                                 log=log)
+    stamps = [t0] + [l["t"] for l in log]
+    dt = stamps[-1] - stamps[1]
+    seeds = sum(min(batch, PARITY_ITEMS - l["batch"] * batch) for l in log[1:])
+    return {"value": 2 * seeds / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu": cpu_info,
+            "sample": f"{iters - 1} timed find_direction iterations after 1 warm-up, batch {batch} "
+                      f"({seeds} seed-steps, FFHQ-{resolution}, CLIP ViT-B/32 + IR-SE50) in {dt:.1f} s: oracle/ "
+                      f"pure-torch fp32 CPU restatement of the reference loop, {threads} threads"}, delta.detach()
 
 
-def direction_parity(G, clip, id_loss, resolution, iters, delta_ref, dev, temp_shapes):
+def direction_parity(G, clip, id_loss, resolution, batch, iters, delta_ref, dev, temp_shapes):
     """The metric's 'dir cosine-sim vs ref': the GPU DirectionFinder run on the cpu_baseline's exact
-    problem (same seeded weights, the same `iters` S codes at batch 1, same batch picks and start point)
-    and its final direction compared with the oracle's."""
+    problem (same seeded weights, S codes, batch, batch picks and start point); final directions compared."""
     from stylemc_amd import synthetic
     from stylemc_amd.find_direction import DirectionFinder, initial_delta
-    styles = synthetic.synthetic_styles(iters, seed=0).to(dev)
-    f = DirectionFinder(G, styles, clip, id_loss, resolution=resolution, batch_size=1, n_epochs=1, seed=0,
-                        init_delta=initial_delta(0, 0.01), temp_shapes=temp_shapes)
+    styles = synthetic.synthetic_styles(PARITY_ITEMS, seed=0).to(dev)
+    init = initial_delta(0, 0.01)
+    f = DirectionFinder(G, styles, clip, id_loss, resolution=resolution, batch_size=batch, n_epochs=PARITY_EPOCHS,
+                        seed=0, init_delta=init, temp_shapes=temp_shapes)
     for _ in range(iters):
         f.step()
     g = f.delta.detach().cpu().double().flatten()
     r = delta_ref.double().flatten()
     cos = torch.nn.functional.cosine_similarity(g, r, dim=0).item()
+    i0 = init.double().flatten()
+    ucos = torch.nn.functional.cosine_similarity(g - i0, r - i0, dim=0).item()
     err = ((g - r).abs().max() / r.abs().max()).item()
-    return {"dir_cosine_vs_oracle": round(cos, 7), "dir_max_rel_err": float(f"{err:.3e}"), "iters": iters,
-            "batch": 1, "target": ">= 0.999",
-            "what": f"final [1,8,512] direction after {iters} find_direction iterations at FFHQ-{resolution}: "
-                    f"HIP path vs oracle/ (fp32 CPU restatement of the reference loop) on identical inputs"}
+    return {"dir_cosine_vs_oracle": round(cos, 7), "update_cosine_vs_oracle": round(ucos, 7),
+            "dir_max_rel_err": float(f"{err:.3e}"), "iters": iters, "batch": batch, "target": ">= 0.999",
+            "what": f"final [1,8,512] direction after {iters} find_direction iterations at FFHQ-{resolution}, "
+                    f"batch {batch}: HIP path vs oracle/ (fp32 CPU restatement of the reference loop, pinned to "
+                    f"the reference by tests/golden) on identical inputs"}
+
+
+def dist_selfcheck(G, clip, id_loss, world, dev, temp_shapes, resolution, batch, steps=2):
+    """N > 1: the N-rank direction after `steps` steps on one global batch vs rank 0 re-running the same global
+    batch in a single process (the all_reduce must reproduce the single-process gradient)."""
+    from stylemc_amd import dist as sdist
+    from stylemc_amd import synthetic
+    from stylemc_amd.find_direction import DirectionFinder, initial_delta
+    B = batch * world.world_size
+    styles = synthetic.synthetic_styles(B, seed=17).to(dev)
+    init = initial_delta(1, 0.01)
+    kw = dict(resolution=resolution, batch_size=B, global_batch=B, n_epochs=4, seed=0, init_delta=init,
+              temp_shapes=temp_shapes)
+    f = DirectionFinder(G, styles, clip, id_loss, world=world, **kw)
+    for _ in range(steps):
+        f.step()
+    d_n = f.delta.detach().cpu().double().flatten()
+    out = None
+    if world.rank == 0:
+        f1 = DirectionFinder(G, styles, clip, id_loss, world=sdist.World(), **kw)
+        for _ in range(steps):
+            f1.step()
+        d_1 = f1.delta.detach().cpu().double().flatten()
+        i0 = init.double().flatten()
+        out = {"dir_cosine_vs_1rank": round(torch.nn.functional.cosine_similarity(d_n, d_1, dim=0).item(), 7),
+               "update_cosine_vs_1rank": round(torch.nn.functional.cosine_similarity(d_n - i0, d_1 - i0, dim=0).item(), 7),
+               "steps": steps, "global_batch": B, "backend": world.backend,
+               "world_size": torch.distributed.get_world_size()}
+    world.barrier()
+    return out
 
 
 def pmc_traffic():
@@ -159,8 +244,7 @@ def main():
     # five a 1-seed global batch that leaves 7 of 8 GPUs idle for that step
     n_seeds = args.n_seeds if args.n_seeds is not None else 129 * world.world_size
     styles = synthetic.synthetic_styles(n_seeds, seed=0).to(dev)
-    clip = build_clip_losses(args.clip_type, dev, "a photo of a face of a feminine woman with no makeup",
-                             "a photo of a face of a masculine man", impl=args.clip_impl)
+    clip = build_clip_losses(args.clip_type, dev, *TEXT, impl=args.clip_impl)
     finder = DirectionFinder(G, styles, clip, IDLoss("a", device=dev, weights=None, impl=args.id_impl), resolution=args.resolution,
                              batch_size=args.batch, global_batch=args.batch * world.world_size, seed=0, world=world,
                              init_delta=initial_delta(0, 0.01), n_epochs=1000,
@@ -206,10 +290,15 @@ def main():
                     "kernel": "conv_gemm_kernel family (synthesis modconv GEMMs)", "launches": s["launches"],
                     "avg_launch_us": round(1e6 * s["seconds"] / max(s["launches"], 1), 2),
                     "alg_gflop_per_launch": round(s["flops"] / max(s["launches"], 1) / 1e9, 3),
+                    "alg_bytes_per_launch": int(s["bytes"] / max(s["launches"], 1)),
                     "share_of_step_time": round(s["seconds"] / dt_r, 4),
                     "measured": f"HIP events around every launch, {args.roofline_steps} serialised steps after the "
                                 f"timed region"}
 
+    selfcheck = None
+    if world.world_size > 1:
+        selfcheck = dist_selfcheck(G, clip, finder.id_loss, world, dev, finder.temp_shapes, args.resolution,
+                                   args.batch)
     if world.rank != 0:
         return
     out = {
@@ -238,12 +327,16 @@ def main():
         "cpu_baseline": None,
         "parity": None,
     }
+    if selfcheck is not None:
+        out["parity"] = selfcheck
     if world.world_size == 1 and not args.no_cpu_baseline:
-        threads = min(args.cpu_threads, os.cpu_count() or 1)
-        out["cpu_baseline"], delta_ref = cpu_baseline(args.resolution, args.cpu_iters, threads)
+        threads, info = host_cpus()
+        if args.cpu_threads > 0:
+            threads = args.cpu_threads
+        out["cpu_baseline"], delta_ref = cpu_baseline(args.resolution, args.cpu_batch, args.cpu_iters, threads, info)
         try:
-            out["parity"] = direction_parity(G, clip, finder.id_loss, args.resolution, args.cpu_iters, delta_ref, dev,
-                                             finder.temp_shapes)
+            out["parity"] = direction_parity(G, clip, finder.id_loss, args.resolution, args.cpu_batch,
+                                             args.cpu_iters, delta_ref, dev, finder.temp_shapes)
         except Exception as e:  # keep the bench line; the failure is reported in it
             out["parity"] = {"error": f"{type(e).__name__}: {e}"}
     print(json.dumps(out), flush=True)

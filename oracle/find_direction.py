@@ -14,6 +14,7 @@ shipped script cannot run: generate_image is called without ``device``, find_dir
     direction instead (stylemc_amd.find_direction.initial_delta).
 """
 import math
+import time
 
 import numpy as np
 import torch
@@ -60,7 +61,7 @@ def find_direction(G, styles_array, clip_loss, id_loss, temp_shapes, until_k, ba
             with torch.no_grad():
                 delta.add_(delta.grad, alpha=-lr_t)
             if log is not None:
-                log.append({"it": it, "batch": i, "lr": lr_t, "loss": float(loss.detach()),
+                log.append({"it": it, "batch": i, "lr": lr_t, "loss": float(loss.detach()), "t": time.perf_counter(),
                             "grad_norm": float(delta.grad.norm()), **{k: float(torch.as_tensor(v).detach()) for k, v in parts.items()}})
             if max_iterations is not None and it >= max_iterations:
                 return styles_direction, delta.detach()

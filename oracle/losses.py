@@ -209,9 +209,14 @@ class IDLoss(nn.Module):
 
 def compute_loss(img, original_img, styles, styles2, clip_loss, id_loss, mean, std,
                  identity_loss_coef=0.6, clip_loss_coef=1.0, l2_reg_coef=0.1,
-                 trainable=(2, 3, 5, 6, 8, 9, 11, 12)):
+                 trainable=(2, 3, 5, 6, 8, 9, 11, 12), clip_loss2=None):
+    """find_direction.py:172-200; clip_loss2 = the ViT-B/16 loss of --clip_type double (:163-166: L32 + 0.5 L16)."""
     identity_loss = id_loss(img, original_img)[0] * identity_loss_coef
-    clip_alignment_loss = clip_loss(unprocess(original_img, mean, std), unprocess(img, mean, std)) * clip_loss_coef
+    src, tgt = unprocess(original_img, mean, std), unprocess(img, mean, std)
+    clip_alignment_loss = clip_loss(src, tgt)
+    if clip_loss2 is not None:
+        clip_alignment_loss = clip_alignment_loss + 0.5 * clip_loss2(src, tgt)
+    clip_alignment_loss = clip_alignment_loss * clip_loss_coef
     t = list(trainable)
     l2 = l2_reg_coef * F.mse_loss(styles2[:, t], styles[:, t])
     loss = identity_loss + clip_alignment_loss + l2

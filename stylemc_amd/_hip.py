@@ -158,24 +158,24 @@ class KernelTimer:
 
     def __init__(self, family):
         self.family = family
-        self.records = []  # (start_event, end_event, flops)
+        self.records = []  # (start_event, end_event, flops, algorithmic bytes)
 
-    def wrap(self, flops):
+    def wrap(self, flops, nbytes=0):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
-        return s, e, flops
+        return s, e, flops, nbytes
 
     def finish(self, token):
-        s, e, flops = token
+        s, e, flops, nbytes = token
         e.record()
-        self.records.append((s, e, flops))
+        self.records.append((s, e, flops, nbytes))
 
     def summary(self):
         torch.cuda.synchronize()
-        times = [s.elapsed_time(e) * 1e-3 for s, e, _ in self.records]
-        flops = [f for _, _, f in self.records]
-        return {"launches": len(times), "seconds": sum(times), "flops": sum(flops)}
+        times = [r[0].elapsed_time(r[1]) * 1e-3 for r in self.records]
+        return {"launches": len(times), "seconds": sum(times), "flops": sum(r[2] for r in self.records),
+                "bytes": sum(r[3] for r in self.records)}
 
 
 _timer = None

@@ -81,6 +81,34 @@ def unprocess(img, mean, std, size=224):
     return (x / 255 - mean) / std
 
 
+def compute_loss(img, original_img, transf, mean, std, device, clip_loss_type, clip_type, clip_loss_coef,
+                 clip_loss1_func, clip_loss2_func, text_prompt, negative_text_prompt, id_loss, identity_loss_coef,
+                 landmarks_loss, landmarks_loss_coef, mobilenet, img_size, styles, styles2, l2_reg_coef):
+    """find_direction.py:172-200 with the reference's signature (unbatched form: each loss network sees the
+    edited and the original image separately; DirectionFinder.step runs the batched equivalent).
+
+    ``transf`` must be None: the torchvision Resize(224, BICUBIC) + CenterCrop of :258 is built into
+    ``unprocess``.  The landmarks term is 0 (computed under no_grad in the reference, :90) and the
+    StyleGAN-NADA losses are out of scope.
+    """
+    if transf is not None:
+        raise ValueError("transf: the bicubic Resize + CenterCrop is built into unprocess(); pass None")
+    if clip_loss_type != "default":
+        raise NotImplementedError("the StyleGAN-NADA losses (clip_loss_nada.py) are outside the hot path")
+    identity_loss = id_loss(img, original_img)[0] * identity_loss_coef
+    tgt = unprocess(img, mean, std, img_size)
+    src = unprocess(original_img, mean, std, img_size)
+    clip_alignment_loss = clip_loss1_func(src, tgt)
+    if clip_type == "double":
+        clip_alignment_loss = clip_alignment_loss + 0.5 * clip_loss2_func(src, tgt)
+    clip_alignment_loss = clip_loss_coef * clip_alignment_loss
+    T = S_TRAINABLE_SPACE_CHANNELS
+    l2 = l2_reg_coef * F.mse_loss(styles2[:, T], styles[:, T])
+    loss = identity_loss + clip_alignment_loss + l2
+    return loss, {"clip_loss": clip_alignment_loss, "identity_loss": identity_loss, "landmarks_loss": 0.0,
+                  "l2_loss": l2}
+
+
 def initial_delta(seed=0, init_std=0.01, device="cpu"):
     """Seeded starting direction [1, 8, 512] (see the module docstring: an exact zero start is NaN)."""
     g = torch.Generator().manual_seed(int(seed) + 7919)

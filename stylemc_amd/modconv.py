@@ -90,14 +90,17 @@ def conv_flops(n, cin, cout, h_out, w_out, taps):
     return 2.0 * n * cin * cout * h_out * w_out * taps
 
 
-def gemm(x, y, phases, nph, cin, cout, s=None, epi=None, alg_flops=0.0):
+def gemm(x, y, phases, nph, cin, cout, s=None, epi=None, alg_flops=0.0, alg_bytes=0):
+    """One smc_conv_gemm_f32 launch.  alg_flops / alg_bytes: the conv's dense MACs x 2 and its compulsory HBM
+    bytes (input and output activations once, weights once, plus the saved u / scaled-input planes) -- only
+    recorded by the bench's KernelTimer."""
     n, _, ih, iw = x.shape
     yh, yw = y.shape[2], y.shape[3]
     lib = _hip.load()
     ws_bytes = lib.smc_conv_gemm_workspace_size(n, cin, cout, yh, yw, phases, nph)
     ws = torch.empty(max(ws_bytes // 4, 1), device=x.device, dtype=torch.float32) if ws_bytes > 0 else None
     tm = _hip.timer()
-    tok = tm.wrap(alg_flops) if tm is not None else None
+    tok = tm.wrap(alg_flops, alg_bytes) if tm is not None else None
     _hip.call("smc_conv_gemm_f32", x.data_ptr(), n, cin, ih, iw, y.data_ptr(), cout, yh, yw, phases, nph,
               _hip.ptr(s), ctypes.byref(epi) if epi is not None else None, _hip.ptr(ws), ws_bytes, _hip.stream())
     if tok is not None:
@@ -164,13 +167,15 @@ class ModConvFn(torch.autograd.Function):
         nz, nstride = _noise_args(noise)
         epi = _epilogue(_hip.EPI_MODACT, d, nz, nstride, strength, spec.bias, spec.act, spec.alpha, gain, clamp, u)
         phases, nph, th, tw = P.fwd_phases(h, w)
+        wbytes = 4 * P.k * P.k * cin * P.cout
         if spec.up == 1:
             gemm(x, y, phases, nph, cin, P.cout, s=styles, epi=epi,
-                 alg_flops=conv_flops(n, cin, P.cout, r_h, r_w, P.k * P.k))
+                 alg_flops=conv_flops(n, cin, P.cout, r_h, r_w, P.k * P.k),
+                 alg_bytes=4 * x.numel() + 4 * y.numel() * (2 if save else 1) + wbytes)
         else:
             t = torch.empty(n, P.cout, th, tw, device=x.device, dtype=torch.float32)
             gemm(x, t, phases, nph, cin, P.cout, s=styles, epi=_epilogue(_hip.EPI_STORE),
-                 alg_flops=conv_flops(n, cin, P.cout, h, w, 9))
+                 alg_flops=conv_flops(n, cin, P.cout, h, w, 9), alg_bytes=4 * x.numel() + 4 * t.numel() + wbytes)
             f = spec.filter.to(x.device)
             fh, fw = f.shape
             _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, P.cout, th, tw, r_h, r_w,
@@ -215,7 +220,8 @@ class ModConvFn(torch.autograd.Function):
             ebw = _epilogue(_hip.EPI_STORE)
             out = dxs
         phases, nph = P.bwd_phases(h, w)
-        gemm(g, out, phases, nph, P.cout, cin, epi=ebw, alg_flops=conv_flops(n, P.cout, cin, h, w, P.k * P.k))
+        gemm(g, out, phases, nph, P.cout, cin, epi=ebw, alg_flops=conv_flops(n, P.cout, cin, h, w, P.k * P.k),
+             alg_bytes=4 * g.numel() + 4 * out.numel() * (2 if (need_dx and need_ds) else 1) + 4 * P.k * P.k * cin * P.cout)
         ds = None
         if need_ds:
             ds = torch.empty(n, cin, device=x.device, dtype=torch.float32)

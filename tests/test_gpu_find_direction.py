@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _run_pair(res, cbase, n_items, bs, iters):
+def _run_pair(res, cbase, n_items, bs, iters, impl="hip"):
     from stylemc_amd import build, networks
     from stylemc_amd.clip_loss import CLIPLoss
     from stylemc_amd.find_direction import DirectionFinder, initial_delta
@@ -41,19 +41,22 @@ def _run_pair(res, cbase, n_items, bs, iters):
     # GPU build
     cfg = synthetic.generator_config(resolution=res, channel_base=cbase)
     G = networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=DEV)
-    f = DirectionFinder(G, styles.to(DEV), [(CLIPLoss(DEV, text_features=text, seed=4), 1.0)],
-                        IDLoss(device=DEV, weights=None, seed=3), resolution=res, batch_size=bs, n_epochs=1, seed=2,
-                        init_delta=init)
+    f = DirectionFinder(G, styles.to(DEV), [(CLIPLoss(DEV, text_features=text, seed=4, impl=impl), 1.0)],
+                        IDLoss(device=DEV, weights=None, seed=3, impl=impl), resolution=res, batch_size=bs,
+                        n_epochs=1, seed=2, init_delta=init)
     parts = []
     for _ in range(iters):
         parts.append(f.step()["parts"].cpu())
-    return (sdir_o, delta_o, log), (f.styles_direction.cpu(), f.delta.cpu(), parts)
+    return (sdir_o, delta_o - init, log), (f.styles_direction.cpu(), f.delta.cpu() - init, parts)
 
 
 def _check(o, g, max_err):
+    """o/g = (saved direction, total update delta_K - delta_0, per-iteration parts): the update vector is the
+    strict comparison (the seeded start would otherwise dominate the cosine after one or two steps)."""
     sdir_o, delta_o, log = o
     sdir_g, delta_g, parts = g
     assert torch.isfinite(delta_g).all()
+    assert len(parts) == len(log)
     for it, (p, l) in enumerate(zip(parts, log)):
         ref = torch.tensor([l["clip_loss"], l["identity_loss"], 0.0, l["l2_loss"]])
         assert torch.allclose(p, ref, rtol=1e-3, atol=1e-5), (it, p, ref)
@@ -72,3 +75,20 @@ def test_find_direction_tiny_generator_vs_oracle():
 
 def test_find_direction_ffhq1024_vs_oracle():
     _check(*_run_pair(1024, 32768, n_items=3, bs=2, iters=2), max_err=1e-2)
+
+
+def test_find_direction_ffhq1024_bs4_vs_oracle():
+    """The headline configuration (BASELINE configs 2-4 per GPU): FFHQ-1024, batch 4, 2 iterations over 5
+    S codes (batches of 4 and the short last batch of 1)."""
+    _check(*_run_pair(1024, 32768, n_items=5, bs=4, iters=2), max_err=1e-2)
+
+
+def test_find_direction_ffhq1024_bs8_vs_oracle():
+    """BASELINE config 4 with the real batch: find_direction --batch_size 8 (16 images per loss network)."""
+    _check(*_run_pair(1024, 32768, n_items=8, bs=8, iters=1), max_err=1e-2)
+
+
+def test_find_direction_ffhq1024_torch_losses_vs_oracle():
+    """BASELINE config 2: CLIP ViT-B/32 and IR-SE50 on PyTorch-ROCm ops (--clip-impl/--id-impl torch), the
+    synthesis on the HIP kernels, forward and backward through the whole loop."""
+    _check(*_run_pair(1024, 32768, n_items=3, bs=2, iters=2, impl="torch"), max_err=1e-2)
