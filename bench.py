@@ -244,7 +244,7 @@ def main():
     # five a 1-seed global batch that leaves 7 of 8 GPUs idle for that step
     n_seeds = args.n_seeds if args.n_seeds is not None else 129 * world.world_size
     styles = synthetic.synthetic_styles(n_seeds, seed=0).to(dev)
-    clip = build_clip_losses(args.clip_type, dev, *TEXT, impl=args.clip_impl)
+    clip = build_clip_losses(args.clip_type, dev, *TEXT, impl=args.clip_impl, synthetic_weights=True)
     finder = DirectionFinder(G, styles, clip, IDLoss("a", device=dev, weights=None, impl=args.id_impl), resolution=args.resolution,
                              batch_size=args.batch, global_batch=args.batch * world.world_size, seed=0, world=world,
                              init_delta=initial_delta(0, 0.01), n_epochs=1000,

@@ -235,6 +235,11 @@ int smc_attention_fwd_f32(const float* qkv, float* out, float* p_save, int batch
                           int head_dim, float scale, void* stream);
 int smc_attention_bwd_f32(const float* dout, const float* qkv, const float* p_save, float* dqkv, int batch,
                           int tokens, int heads, int head_dim, float scale, void* stream);
+/* The same forward with the causal mask of CLIP's text transformer (openai/CLIP model.py
+ * build_attention_mask: -inf above the diagonal), used once per prompt by the CLIPLoss text side
+ * (clip_loss.py:15-18 encode_text).  Forward only. */
+int smc_attention_causal_fwd_f32(const float* qkv, float* out, int batch, int tokens, int heads, int head_dim,
+                                 float scale, void* stream);
 
 /* Non-overlapping patch extraction (conv kernel == stride): img [batch][channels][grid*patch]^2 <->
  * patches [batch*grid*grid][channels*patch*patch]; inverse = 1 writes img from patches. */

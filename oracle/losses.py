@@ -110,6 +110,45 @@ class CLIPVisual(nn.Module):
         return self.ln_post(x[:, 0, :]) @ self.proj
 
 
+class _TextResBlock(_ResBlock):
+    def __init__(self, d, heads, mask):
+        super().__init__(d, heads)
+        self.register_buffer("attn_mask", mask, persistent=False)
+
+    def forward(self, x):  # x: [L, N, D]
+        h = self.ln_1(x)
+        x = x + self.attn(h, h, h, need_weights=False, attn_mask=self.attn_mask)[0]
+        return x + self.mlp(self.ln_2(x))
+
+
+class CLIPText(nn.Module):
+    """openai/CLIP text encoder (model.py encode_text; third-party, PARITY UNPINNED): token + positional
+    embedding, residual blocks under the causal mask (build_attention_mask: -inf above the diagonal),
+    ln_final, the EOT token's row (text.argmax(-1)) @ text_projection.  Keys == the CLIP model's text keys."""
+
+    def __init__(self, embed_dim=512, context_length=77, vocab_size=49408, width=512, heads=8, layers=12):
+        super().__init__()
+        mask = torch.full((context_length, context_length), float("-inf")).triu_(1)
+        self.token_embedding = nn.Embedding(vocab_size, width)
+        self.positional_embedding = nn.Parameter(torch.empty(context_length, width))
+        self.transformer = nn.Module()
+        self.transformer.resblocks = nn.Sequential(*[_TextResBlock(width, heads, mask) for _ in range(layers)])
+        self.ln_final = _LayerNorm(width)
+        self.text_projection = nn.Parameter(torch.empty(width, embed_dim))
+
+    def forward(self, text):
+        x = self.token_embedding(text) + self.positional_embedding
+        x = self.transformer.resblocks(x.permute(1, 0, 2)).permute(1, 0, 2)
+        x = self.ln_final(x)
+        return x[torch.arange(x.shape[0]), text.argmax(dim=-1)] @ self.text_projection
+
+
+def text_features(text_model, tokens_pos, tokens_neg):
+    """clip_loss.py:15-18: norm(E_T(pos) - E_T(neg))."""
+    t = text_model(tokens_pos) - text_model(tokens_neg)
+    return t / t.norm(dim=1, keepdim=True)
+
+
 class CLIPLoss(nn.Module):
     """Directional CLIP loss (clip_loss.py:24-34) around an image encoder and a text direction."""
 

@@ -76,6 +76,7 @@ _SIGS = {
     "smc_layernorm_bwd_f32": (c_int, [P, c_int64, P, c_int64, P, P, P, P, c_int64, P, c_int64, c_int, c_int, P]),
     "smc_attention_fwd_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_float, P]),
     "smc_attention_bwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, P]),
+    "smc_attention_causal_fwd_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, c_float, P]),
     "smc_patch_im2col_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "smc_vit_packed_floats": (c_int64, [P]),
     "smc_vit_saved_floats": (c_int64, [P, c_int]),

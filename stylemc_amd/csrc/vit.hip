@@ -508,7 +508,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* dy, int64_t ld
 constexpr int HD = 64, HP = 65, AQB = 16, AQB_BWD_SINGLE = 64;
 
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* qkv, float* out, float* psave, int L, int H,
-                                                       float scale) {
+                                                       float scale, int causal) {
     extern __shared__ float sm[];
     float* Ks = sm;
     float* Vs = Ks + L * HP;
@@ -534,7 +534,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* qkv, float* 
         float s = 0.f;
 #pragma unroll 16
         for (int d = 0; d < HD; ++d) s = fmaf(Qs[i * HP + d], Ks[j * HP + d], s);
-        Ss[i * L + j] = s;
+        // causal: the -inf upper triangle of CLIP's text mask (attn_mask triu(1)); exp -> exactly 0
+        Ss[i * L + j] = (causal && j > q0 + i) ? -INFINITY : s;
     }
     __syncthreads();
     for (int i = wave; i < nq; i += 4) {
@@ -656,12 +657,13 @@ int attn_check_lds(size_t bytes, const void* fn) {
     return SMC_OK;
 }
 
-int attn_fwd_launch(const float* qkv, float* out, float* psave, int B, int L, int H, float scale, hipStream_t st) {
+int attn_fwd_launch(const float* qkv, float* out, float* psave, int B, int L, int H, float scale, hipStream_t st,
+                    int causal = 0) {
     const size_t lds = attn_fwd_lds(L);
     int rc = attn_check_lds(lds, reinterpret_cast<const void*>(attn_fwd_kernel));
     if (rc != SMC_OK) return rc;
     hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)smc::ceil_div(L, AQB), H, B), dim3(256), lds, st, qkv, out,
-                       psave, L, H, scale);
+                       psave, L, H, scale, causal);
     return smc::check_launch("smc_attention_fwd_f32");
 }
 
@@ -1017,6 +1019,16 @@ SMC_API int smc_attention_fwd_f32(const float* qkv, float* out, float* p_save, i
         return SMC_ERR_UNSUPPORTED;
     }
     return attn_fwd_launch(qkv, out, p_save, batch, tokens, heads, scale, smc::as_stream(stream));
+}
+
+SMC_API int smc_attention_causal_fwd_f32(const float* qkv, float* out, int batch, int tokens, int heads,
+                                         int head_dim, float scale, void* stream) {
+    SMC_CHECK(qkv && out && batch >= 1 && tokens >= 1 && heads >= 1, "smc_attention_causal_fwd_f32: bad arguments");
+    if (head_dim != HD) {
+        smc::set_error("smc_attention_causal_fwd_f32: head_dim %d (only 64)", head_dim);
+        return SMC_ERR_UNSUPPORTED;
+    }
+    return attn_fwd_launch(qkv, out, nullptr, batch, tokens, heads, scale, smc::as_stream(stream), 1);
 }
 
 SMC_API int smc_attention_bwd_f32(const float* dout, const float* qkv, const float* p_save, float* dqkv, int batch,

@@ -161,6 +161,7 @@ class DirectionFinder:
         # GPU on every use, a blocking copy that drains the stream mid-step
         self.t_idx = torch.tensor(T, dtype=torch.long, device=self.device)
         self.delta = self.styles_direction[:, T].clone()
+        self._offset = None
         if init_delta is not None:
             self.delta = init_delta.detach().to(self.device, torch.float32).reshape(1, len(T), 512).clone()
         self.mean, self.std = utils.get_mean_std(self.device)
@@ -168,10 +169,21 @@ class DirectionFinder:
         self.last = None
 
     def load_direction(self, direction):
-        """--resume: start from a saved [1, 26, 512] direction (the reference's :266-268, fixed)."""
+        """--resume: start from a saved [1, 26, 512] direction (the reference's :266-271, with its
+        ``map_location`` TypeError fixed).  The reference adds the WHOLE styles_direction to the styles
+        (styles2 = styles + styles_direction, :307-308) and trains only the T rows, so any non-zero non-T rows
+        of the resumed file stay a constant offset of the edited image's S codes (and are saved back)."""
         d = torch.as_tensor(direction, dtype=torch.float32, device=self.device).reshape(1, N_STYLE_CHANNELS, 512)
         self.styles_direction.copy_(d)
         self.delta = d[:, S_TRAINABLE_SPACE_CHANNELS].clone()
+        off = d.clone()
+        off[:, S_TRAINABLE_SPACE_CHANNELS] = 0
+        self._offset = off if bool(off.ne(0).any()) else None
+
+    def _edited(self, styles):
+        """The edited image's S codes before the trainable rows: styles + the constant non-T rows of a
+        resumed direction (none for a fresh run)."""
+        return styles if self._offset is None else styles + self._offset
 
     def _original_branch(self, styles):
         """Everything that depends only on the original image (no gradient): its synthesis, its IR-SE50
@@ -191,7 +203,7 @@ class DirectionFinder:
         pref, self._pref = self._pref, None
         if side is not None and pref is not None and pref[0] == key:
             main = torch.cuda.current_stream()
-            img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+            img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
             main.wait_stream(self._pre)
             orig = pref[1]
             orig.record_stream(main)
@@ -200,11 +212,11 @@ class DirectionFinder:
             side.wait_stream(main)
             with torch.cuda.stream(side), torch.no_grad():
                 orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
-            img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+            img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
             main.wait_stream(side)
             orig.record_stream(main)
         else:
-            img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+            img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
             with torch.no_grad():
                 orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
         if side is not None:
@@ -246,12 +258,12 @@ class DirectionFinder:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 y_feats, src_embs = self._original_branch(styles)
-            img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+            img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
             main.wait_stream(side)
             for t in [y_feats] + src_embs:
                 t.record_stream(main)
         else:
-            img = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode, delta=d)
+            img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
             y_feats, src_embs = self._original_branch(styles)
         id_terms = self.id_loss.per_sample_with(img, y_feats)
         tgt = unprocess(img, self.mean, self.std)
@@ -332,27 +344,39 @@ class DirectionFinder:
 # ------------------------------------------------------------------------------------------- CLI helpers
 
 
-def load_generator(network, resolution, device):
-    """'synthetic' -> seeded config-f generator; *.pkl -> the pickle's G_ema through the exec-free unpickler
-    (stylemc_amd.legacy); *.pt/*.pth/*.safetensors -> state_dict (legacy.py:172-203 names)."""
+def load_generator(network, resolution, device, conv_clamp=256):
+    """'synthetic' -> seeded config-f / paper256 generator of ``resolution`` px; *.pkl -> the pickle's G_ema
+    through the exec-free unpickler (stylemc_amd.legacy, config from its init_kwargs); *.pt/*.pth/
+    *.safetensors -> a G_ema state_dict (legacy.py:172-203 names) with the config inferred from its shapes
+    (``conv_clamp`` is not stored there).  For a real network ``resolution`` is NOT the generator's size: as
+    in the reference it only selects how many blocks are rendered (until_k, find_direction.py:263)."""
     from . import legacy, networks, synthetic
-    cfg = synthetic.generator_config(resolution=resolution)
     if network in (None, "", "synthetic"):
+        cfg = synthetic.generator_config(resolution=resolution)
         return networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=device)
     if network.startswith("http"):
         raise SystemExit(f"{network}: no network access; download the pickle and pass its local path")
+    if not os.path.exists(network):
+        raise SystemExit(f"{network}: no such file")
     if network.endswith(".pkl"):
-        G = legacy.load_generator_pkl(network, device=device)
-        if G.img_resolution != resolution:
-            raise SystemExit(f"{network}: generator resolution {G.img_resolution} != --resolution {resolution}")
-        return G
+        return legacy.load_generator_pkl(network, device=device)
     if network.endswith(".safetensors"):
         from safetensors.torch import load_file
         sd = load_file(network)
     else:
         sd = torch.load(network, map_location="cpu", weights_only=True)
     sd = {k[len("G_ema."):] if k.startswith("G_ema.") else k: v for k, v in sd.items()}
-    return networks.build_generator(cfg, sd, device=device)
+    return networks.build_generator(networks.infer_generator_config(sd, conv_clamp), sd, device=device)
+
+
+def until_k_for(G, resolution):
+    """Last block index rendered for --resolution (find_direction.py:263 resolution_dict {256: 6, 512: 7,
+    1024: 8}, i.e. log2(resolution) - 2), bounded by the generator's own depth."""
+    k = RESOLUTION_DICT.get(resolution, int(math.log2(resolution)) - 2)
+    last = len(G.synthesis.block_resolutions) - 1
+    if k > last:
+        raise SystemExit(f"--resolution {resolution} is above the generator's {G.img_resolution} px")
+    return k
 
 
 def load_styles(s_input, n_seeds, device, seed=0):
@@ -362,14 +386,44 @@ def load_styles(s_input, n_seeds, device, seed=0):
     return synthetic.synthetic_styles(n_seeds, seed=seed).to(device)
 
 
-def build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip_loss_type="default", impl="hip"):
+def _load_weights(path):
+    """A state_dict file without code execution: safetensors, or torch.load(weights_only=True)."""
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        return load_file(path)
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
+        sd = sd["state_dict"]
+    return sd
+
+
+def load_text_features(path):
+    """--text_features npz: key 'small' / 'large' per CLIP model, or 'text_features' for both (each
+    [1, 512] = norm(E_T(pos) - E_T(neg)) of that model, clip_loss.py:15-18)."""
+    with np.load(path) as z:
+        if "text_features" in z:
+            return {"small": z["text_features"], "large": z["text_features"]}
+        return {k: z[k] for k in ("small", "large") if k in z}
+
+
+def build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip_loss_type="default", impl="hip",
+                      clip_weights=None, text_features=None, bpe_path=None, synthetic_weights=False):
+    """init_clip_loss (find_direction.py:100-122) for the default loss: [(CLIPLoss, weight)], 'double' ->
+    ViT-B/32 at 1 + ViT-B/16 at 0.5 (:163-166).  clip_weights / text_features: {'small'|'large': ...}."""
     from .clip_loss import CLIPLoss
     if clip_loss_type != "default":
         raise NotImplementedError("the StyleGAN-NADA losses (clip_loss_nada.py) are outside the hot path")
-    if clip_type == "double":
-        return [(CLIPLoss(device, text_prompt, negative_text_prompt, "small", impl=impl), 1.0),
-                (CLIPLoss(device, text_prompt, negative_text_prompt, "large", impl=impl), 0.5)]
-    return [(CLIPLoss(device, text_prompt, negative_text_prompt, clip_type, impl=impl), 1.0)]
+    kinds = [("small", 1.0), ("large", 0.5)] if clip_type == "double" else [(clip_type, 1.0)]
+    clip_weights = clip_weights or {}
+    text_features = text_features or {}
+    out = []
+    for kind, w in kinds:
+        path = clip_weights.get(kind)
+        out.append((CLIPLoss(device, text_prompt, negative_text_prompt, kind, impl=impl,
+                             clip_state_dict=_load_weights(path) if path else None,
+                             text_features=text_features.get(kind), bpe_path=bpe_path,
+                             synthetic_weights=synthetic_weights), w))
+    return out
 
 
 def _cli():
@@ -399,22 +453,44 @@ def _cli():
     @click.option("--per_gpu_batch", is_flag=True, help="throughput mode: global batch = batch_size x world")
     @click.option("--max_iterations", type=int, default=None)
     @click.option("--init_std", type=float, default=0.01, help="std of the seeded start direction (0 = reference)")
+    @click.option("--clip_weights", type=str, default=None, help="OpenAI CLIP ViT-B/32 state_dict (.pt/.safetensors)")
+    @click.option("--clip_weights_large", type=str, default=None, help="OpenAI CLIP ViT-B/16 state_dict (clip_type large/double)")
+    @click.option("--clip_bpe", type=str, default=None, help="CLIP BPE merges file (bpe_simple_vocab_16e6.txt.gz)")
+    @click.option("--text_features", type=str, default=None, help="npz of precomputed text directions ('small'/'large')")
+    @click.option("--id_weights", type=str, default="id_loss/model_ir_se50.pth", show_default=True)
+    @click.option("--conv_clamp", type=float, default=256.0, help="conv_clamp of a state_dict network (not stored in it)")
+    @click.option("--allow_synthetic_losses", is_flag=True,
+                  help="seeded synthetic CLIP / IR-SE50 weights (implied by --network synthetic)")
+    @click.option("--impl", type=click.Choice(["hip", "torch"]), default="hip",
+                  help="loss networks on the gfx950 kernels (hip) or PyTorch-ROCm ops (torch)")
     def find_direction(ctx, network_pkl, noise_mode, s_input, outdir, text_prompt, negative_text_prompt, clip_type,
                        clip_loss_type, resolution, batch_size, learning_rate, n_epochs, resume, identity_loss_coef,
                        landmarks_loss_coef, l2_reg_coef, clip_loss_coef, n_seeds, seed, per_gpu_batch, max_iterations,
-                       init_std):
+                       init_std, clip_weights, clip_weights_large, clip_bpe, text_features, id_weights, conv_clamp,
+                       allow_synthetic_losses, impl):
         from .id_loss import IDLoss
         world = _dist.init_from_env(use_cuda=True)
         device = torch.device("cuda", world.device_index)
         torch.cuda.set_device(device)
         if landmarks_loss_coef != 0:
             warnings.warn("landmarks loss adds no gradient in the reference (no_grad, find_direction.py:90); ignored")
-        G = load_generator(network_pkl, resolution if network_pkl == "synthetic" else 1024, device)
+        synthetic_losses = allow_synthetic_losses or network_pkl in (None, "", "synthetic")
+        G = load_generator(network_pkl, resolution, device, conv_clamp=conv_clamp)
+        until_k_for(G, resolution)
         os.makedirs(outdir, exist_ok=True)
         styles_array = load_styles(s_input, n_seeds, device)
+        clips = build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip_loss_type, impl=impl,
+                                  clip_weights={"small": clip_weights, "large": clip_weights_large},
+                                  text_features=load_text_features(text_features) if text_features else None,
+                                  bpe_path=clip_bpe, synthetic_weights=synthetic_losses)
+        if synthetic_losses and not os.path.exists(id_weights or ""):
+            id_weights = None
+            if world.rank == 0:
+                warnings.warn("IR-SE50 / CLIP: seeded synthetic weights where none were given (synthetic run)")
         finder = DirectionFinder(
-            G, styles_array, build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip_loss_type),
-            IDLoss("a", device=device), resolution=resolution, batch_size=batch_size, learning_rate=learning_rate,
+            G, styles_array, clips,
+            IDLoss("a", device=device, weights=id_weights, impl=impl), resolution=resolution, batch_size=batch_size,
+            learning_rate=learning_rate,
             n_epochs=n_epochs, identity_loss_coef=identity_loss_coef, l2_reg_coef=l2_reg_coef,
             clip_loss_coef=clip_loss_coef, noise_mode=noise_mode, seed=seed, world=world,
             global_batch=batch_size * world.world_size if per_gpu_batch else batch_size,

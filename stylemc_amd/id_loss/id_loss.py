@@ -48,8 +48,14 @@ class IDLoss(nn.Module):
                  impl="hip"):
         super().__init__()
         if facenet is None:
+            # like the reference (id_loss.py:12) a missing weights file is an error; weights=None asks for the
+            # seeded synthetic IR-SE50 explicitly (tests, bench, --network synthetic)
             sd = None
-            if weights and os.path.exists(weights):
+            if weights is not None:
+                if not os.path.exists(weights):
+                    raise FileNotFoundError(f"{weights}: IR-SE50 ArcFace weights not found (the reference loads "
+                                            f"id_loss/model_ir_se50.pth, id_loss.py:12); pass --id_weights, or "
+                                            f"weights=None for seeded synthetic weights")
                 sd = torch.load(weights, map_location="cpu", weights_only=True)
             if impl == "hip":
                 from ..irse_hip import build_irse50 as build_hip

@@ -86,6 +86,13 @@ def _rebuild_parameter_with_state(data, requires_grad, backward_hooks, state):
     return data
 
 
+def _codecs_encode(obj, encoding="utf-8", errors="strict"):
+    """Protocol-2 bytes: _codecs.encode(latin-1 str, 'latin1') (only str -> bytes, nothing else)."""
+    if not isinstance(obj, str):
+        raise pickle.UnpicklingError("_codecs.encode of a non-str")
+    return obj.encode(encoding, errors)
+
+
 class SafeNetworkUnpickler(pickle.Unpickler):
     _ALLOWED = {
         _PERSISTENT: PersistentStub,
@@ -97,6 +104,16 @@ class SafeNetworkUnpickler(pickle.Unpickler):
         ("collections", "OrderedDict"): collections.OrderedDict,
         ("dnnlib.util", "EasyDict"): dict,
         ("builtins", "object"): object,
+        # nn.Module.__dict__ holds _non_persistent_buffers_set: under pickle protocol <= 3 (the official
+        # pickles: Python 3.7, default protocol 3) a set is a REDUCE of builtins.set; protocol 2 names the
+        # Python 2 module and encodes bytes through _codecs.encode
+        ("builtins", "set"): set,
+        ("builtins", "frozenset"): frozenset,
+        ("__builtin__", "set"): set,
+        ("__builtin__", "frozenset"): frozenset,
+        ("__builtin__", "object"): object,
+        ("copy_reg", "_reconstructor"): _reconstructor,
+        ("_codecs", "encode"): _codecs_encode,
         ("numpy", "dtype"): np.dtype,
         ("numpy.core.multiarray", "scalar"): _np_ma.scalar,
         ("numpy.core.multiarray", "_reconstruct"): _np_ma._reconstruct,
@@ -132,9 +149,10 @@ def load_network_pkl(f):
 def _named_tensors(obj, prefix=""):
     """Flatten a stub tree into (name, tensor) like nn.Module.state_dict (parameters, then buffers)."""
     state = obj.state
+    skip = set(state.get("_non_persistent_buffers_set") or ())   # not in state_dict (nn.Module semantics)
     for key in ("_parameters", "_buffers"):
         for name, t in (state.get(key) or {}).items():
-            if t is not None:
+            if t is not None and not (key == "_buffers" and name in skip):
                 yield prefix + name, t
     for name, child in (state.get("_modules") or {}).items():
         if child is not None:

@@ -248,10 +248,35 @@ class Generator(torch.nn.Module):
         return self.synthesis(ws, **synthesis_kwargs)
 
 
+def infer_generator_config(state_dict, conv_clamp=256):
+    """Generator config from a G_ema state_dict's shapes (legacy.py:172-203 names): img_resolution from the
+    highest ``synthesis.b{R}`` block, per-block widths -> channel_base / channel_max, z_dim / w_dim / mapping
+    depth from the mapping and affine FCs.  conv_clamp is not stored in a state_dict (the stylegan2-ada
+    training configs use 256; converted TF-era networks use None)."""
+    import re
+    res = sorted({int(m.group(1)) for k in state_dict for m in [re.match(r"synthesis\.b(\d+)\.", k)] if m})
+    if not res or res[0] != 4:
+        raise KeyError("not a StyleGAN2 generator state_dict (no synthesis.b4.* keys)")
+    R = res[-1]
+    ch = {r: int(state_dict[f"synthesis.b{r}.conv1.weight"].shape[0]) for r in res}
+    channel_max = max(ch.values())
+    below = [ch[r] * r for r in res if ch[r] < channel_max]
+    channel_base = min(below) if below else channel_max * R
+    if any(min(channel_base // r, channel_max) != ch[r] for r in res):
+        raise ValueError(f"block widths {ch} do not follow min(channel_base / r, channel_max)")
+    w_dim = int(state_dict["synthesis.b4.conv1.affine.weight"].shape[1])
+    n_map = len({k.split(".")[1] for k in state_dict if re.match(r"mapping\.fc\d+\.weight$", k)})
+    z_dim = int(state_dict["mapping.fc0.weight"].shape[1]) if n_map else 512
+    return dict(z_dim=z_dim, c_dim=0, w_dim=w_dim, img_resolution=R,
+                img_channels=int(state_dict[f"synthesis.b{R}.torgb.weight"].shape[0]), channel_base=channel_base,
+                channel_max=channel_max, conv_clamp=conv_clamp, mapping_layers=n_map or 8)
+
+
 def build_generator(cfg, state_dict=None, device="cuda"):
     """Generator from a ``synthetic.generator_config`` dict (+ optional state_dict), frozen, on ``device``."""
     G = Generator(cfg["z_dim"], cfg["c_dim"], cfg["w_dim"], cfg["img_resolution"], cfg["img_channels"],
-                  channel_base=cfg["channel_base"], channel_max=cfg["channel_max"], conv_clamp=cfg["conv_clamp"])
+                  mapping_kwargs=dict(num_layers=cfg.get("mapping_layers", 8)), channel_base=cfg["channel_base"],
+                  channel_max=cfg["channel_max"], conv_clamp=cfg["conv_clamp"])
     if state_dict is not None:
         res = G.load_state_dict(state_dict, strict=False)
         bad = [k for k in res.missing_keys if not k.endswith("resample_filter")]

@@ -313,6 +313,70 @@ def gen_clip():
     save("clip_vit_b32_hf.npz", {"x": x, "y": y})
 
 
+def gen_clip_text():
+    """The oracle's CLIP text encoder vs transformers.CLIPTextModelWithProjection (causal mask, quick_gelu,
+    EOS pooling) with the same seeded weights -- an architecture cross-check (openai/CLIP is absent)."""
+    from transformers import CLIPTextConfig, CLIPTextModelWithProjection
+    from oracle.losses import CLIPText
+    ours = CLIPText().eval()
+    sd = synthetic.seeded_state_dict(ours, seed=6)
+    ours.load_state_dict(sd)
+    cfg = CLIPTextConfig(vocab_size=49408, hidden_size=512, intermediate_size=2048, projection_dim=512,
+                         num_hidden_layers=12, num_attention_heads=8, max_position_embeddings=77,
+                         hidden_act="quick_gelu", layer_norm_eps=1e-5, eos_token_id=49407, bos_token_id=49406,
+                         pad_token_id=0)
+    hf = CLIPTextModelWithProjection(cfg).eval()
+    t = "text_model."
+    hsd = {t + "embeddings.token_embedding.weight": sd["token_embedding.weight"],
+           t + "embeddings.position_embedding.weight": sd["positional_embedding"],
+           t + "final_layer_norm.weight": sd["ln_final.weight"], t + "final_layer_norm.bias": sd["ln_final.bias"],
+           "text_projection.weight": sd["text_projection"].t().contiguous()}
+    for i in range(12):
+        o, h = f"transformer.resblocks.{i}.", f"{t}encoder.layers.{i}."
+        for n, (w, b) in zip(("q", "k", "v"), zip(sd[o + "attn.in_proj_weight"].chunk(3), sd[o + "attn.in_proj_bias"].chunk(3))):
+            hsd[f"{h}self_attn.{n}_proj.weight"], hsd[f"{h}self_attn.{n}_proj.bias"] = w, b
+        hsd[h + "self_attn.out_proj.weight"] = sd[o + "attn.out_proj.weight"]
+        hsd[h + "self_attn.out_proj.bias"] = sd[o + "attn.out_proj.bias"]
+        for a, b in (("ln_1", "layer_norm1"), ("ln_2", "layer_norm2")):
+            hsd[h + b + ".weight"], hsd[h + b + ".bias"] = sd[o + a + ".weight"], sd[o + a + ".bias"]
+        hsd[h + "mlp.fc1.weight"], hsd[h + "mlp.fc1.bias"] = sd[o + "mlp.c_fc.weight"], sd[o + "mlp.c_fc.bias"]
+        hsd[h + "mlp.fc2.weight"], hsd[h + "mlp.fc2.bias"] = sd[o + "mlp.c_proj.weight"], sd[o + "mlp.c_proj.bias"]
+    res = hf.load_state_dict(hsd, strict=False)
+    assert not res.unexpected_keys and all("position_ids" in k for k in res.missing_keys), res
+    g = torch.Generator().manual_seed(14)
+    tokens = torch.zeros(3, 77, dtype=torch.long)
+    for i, n in enumerate((5, 12, 75)):
+        tokens[i, 0] = 49406
+        tokens[i, 1:n + 1] = torch.randint(1, 49405, (n,), generator=g)
+        tokens[i, n + 1] = 49407
+    with torch.no_grad():
+        y = hf(input_ids=tokens).text_embeds
+        y_ours = ours(tokens)
+    print("oracle vs HF text tower max |diff|", (y - y_ours).abs().max().item())
+    save("clip_text_hf.npz", {"tokens": tokens, "y": y})
+
+
+def gen_mapper():
+    """latent_mappers.Mapper of the REFERENCE (latent_mappers.py:12-93, with e4e's PixelNorm from
+    encoder4editing/models/stylegan2/model.py:10-15) on seeded weights; the e4e CUDA op package (JIT-built
+    at import) and torchvision are import-only stubs -- the mapper never calls them."""
+    tv = _stub("torchvision")
+    tv.transforms = _stub("torchvision.transforms", Compose=_Absent, Resize=_Absent, CenterCrop=_Absent)
+    _stub("encoder4editing.models.stylegan2.op", FusedLeakyReLU=_Absent, fused_leaky_relu=_Absent, upfirdn2d=_Absent)
+    import latent_mappers as ref_lm
+    out = {}
+    for slope in (0.01, 0.2):
+        m = ref_lm.Mapper(neg_slope=slope).eval()
+        sd = synthetic.seeded_state_dict(m, seed=8)
+        m.load_state_dict(sd)
+        x = synthetic.synthetic_styles(3, seed=8)[:, [2, 3, 5, 6, 8, 9, 11, 12]]
+        with torch.no_grad():
+            y = m(x)
+        out[f"s{slope}/y"] = y
+    out["x"] = x
+    save("mapper.npz", out)
+
+
 # ---------------------------------------------------------------------------------- loss composition + loop
 
 

@@ -27,6 +27,7 @@ def _run_pair(res, cbase, n_items, bs, iters, impl="hip"):
     text = synthetic.text_direction("a photo of a face of a feminine woman", "a photo of a face of a man")
     styles = synthetic.synthetic_styles(n_items, seed=5)
     init = initial_delta(0, 0.01)
+    n_epochs = -(-iters // -(-n_items // bs))   # enough epochs for `iters` iterations (same lr schedule both sides)
     # CPU oracle
     Go = oracle_generator(res, cbase, seed=0)
     vis = OL.CLIPVisual().eval()
@@ -36,14 +37,14 @@ def _run_pair(res, cbase, n_items, bs, iters, impl="hip"):
     log = []
     sdir_o, delta_o = OF.find_direction(Go, styles, OL.CLIPLoss(vis.requires_grad_(False), text),
                                         OL.IDLoss(net.requires_grad_(False)), OS.get_temp_shapes(Go),
-                                        res.bit_length() - 3, batch_size=bs, n_epochs=1, seed=2,
+                                        res.bit_length() - 3, batch_size=bs, n_epochs=n_epochs, seed=2,
                                         max_iterations=iters, log=log, init_delta=init)
     # GPU build
     cfg = synthetic.generator_config(resolution=res, channel_base=cbase)
     G = networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=DEV)
-    f = DirectionFinder(G, styles.to(DEV), [(CLIPLoss(DEV, text_features=text, seed=4, impl=impl), 1.0)],
+    f = DirectionFinder(G, styles.to(DEV), [(CLIPLoss(DEV, text_features=text, synthetic_weights=True, seed=4, impl=impl), 1.0)],
                         IDLoss(device=DEV, weights=None, seed=3, impl=impl), resolution=res, batch_size=bs,
-                        n_epochs=1, seed=2, init_delta=init)
+                        n_epochs=n_epochs, seed=2, init_delta=init)
     parts = []
     for _ in range(iters):
         parts.append(f.step()["parts"].cpu())

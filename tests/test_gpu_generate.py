@@ -75,3 +75,32 @@ def test_seeds_to_w_to_s_vs_oracle():
     s_o, _ = OS.get_styles(Go, ws_o)
     assert s.shape == (3, 26, 512)
     np.testing.assert_allclose(s.cpu().numpy(), s_o.numpy(), rtol=1e-4, atol=1e-4 * s_o.abs().max().item())
+
+
+@pytest.mark.parametrize("use_whitelist", [False, True])
+def test_generate_fromS_mapper_vs_oracle(use_whitelist):
+    """--use_mapper 1 (generate_fromS.py:117-122,149-165): per-item direction from the latent mapper."""
+    from stylemc_amd import generate_fromS, utils
+    from stylemc_amd.latent_mappers import Mapper
+    G, Go = _pair(32, 512)
+    m = Mapper(neg_slope=0.01).eval()
+    m.load_state_dict(synthetic.seeded_state_dict(m, seed=8))
+    styles = synthetic.synthetic_styles(3, seed=4)
+    got = list(generate_fromS.render_pairs(G, styles.to(DEV), None, 3.0, utils.get_temp_shapes(G),
+                                           mapper=m.to(DEV), use_whitelist=use_whitelist))
+    ref = OG.render_pairs(Go, styles.clone(), None, 3.0, OS.get_temp_shapes(Go), mapper=m.cpu(),
+                          use_whitelist=use_whitelist)
+    for (i, imgs), rimgs in zip(got, ref):
+        for k in range(2):
+            _check_u8(imgs[k], rimgs[k], f"item {i} power {k}")
+
+
+def test_generate_fromS_projected_w_vs_oracle():
+    """--projected-w (generate_fromS.py:89-102): G.synthesis(w) for each W row, uint8 per-pixel."""
+    from stylemc_amd import generate_fromS, w_s
+    G, Go = _pair(1024, 32768)
+    ws = w_s.seeds_to_w(G, [5, 6], truncation_psi=0.7)
+    got = [img for _, img in generate_fromS.render_projected_w(G, ws)]
+    ref = OG.render_projected_w(Go, ws.cpu())
+    for a, b in zip(got, ref):
+        _check_u8(a, b, "projected w")

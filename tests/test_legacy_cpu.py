@@ -13,6 +13,7 @@ import pickle
 import sys
 import types
 
+import numpy as np
 import pytest
 import torch
 
@@ -46,19 +47,19 @@ class _Persistent:
 
 
 def _as_persistent(module, fn, init_kwargs=None):
-    state = {
-        "training": False,
-        "_parameters": collections.OrderedDict((k, v) for k, v in module._parameters.items() if v is not None),
-        "_buffers": collections.OrderedDict((k, v) for k, v in module._buffers.items() if v is not None),
-        "_modules": collections.OrderedDict((k, _as_persistent(m, fn)) for k, m in module._modules.items()
-                                            if m is not None),
-    }
+    """persistence.py:119-127: the persistent object's state is the module's WHOLE __dict__ (hook
+    OrderedDicts, _non_persistent_buffers_set, plain attributes, numpy scalars, ...)."""
+    # (this package's own per-layer kernel caches are not part of an upstream layer's __dict__)
+    state = {k: v for k, v in module.__dict__.items() if not type(v).__module__.startswith("stylemc_amd")}
+    state["training"] = False
+    state["_modules"] = collections.OrderedDict((k, _as_persistent(m, fn)) for k, m in module._modules.items()
+                                                if m is not None)
     if init_kwargs is not None:
         state["_init_kwargs"] = init_kwargs
     return _Persistent(fn, type(module).__name__, state)
 
 
-def _make_pickle(G, init_kwargs, extra=None):
+def _make_pickle(G, init_kwargs, extra=None, protocol=4):
     pkg, mod = _fake_persistence_module()
     saved = {k: sys.modules.get(k) for k in ("torch_utils", "torch_utils.persistence")}
     sys.modules["torch_utils"], sys.modules["torch_utils.persistence"] = pkg, mod
@@ -68,7 +69,7 @@ def _make_pickle(G, init_kwargs, extra=None):
                    G_ema=_as_persistent(G, fn, init_kwargs), training_set_kwargs=None, augment_pipe=None)
         if extra:
             top.update(extra)
-        return pickle.dumps(top, protocol=4)
+        return pickle.dumps(top, protocol=protocol)
     finally:
         for k, v in saved.items():
             if v is None:
@@ -86,11 +87,20 @@ def _generator(res=32, cbase=512):
     return G, kw
 
 
-def test_roundtrip_state_and_config(tmp_path):
+@pytest.mark.parametrize("protocol", [2, 3, 4])
+def test_roundtrip_state_and_config(tmp_path, protocol):
+    """Protocol 3 is what the official pickles use (Python 3.7 default); 2 and 4 for completeness."""
     G, kw = _generator()
+    G.synthesis.b8.conv1.weight_gain_np = np.float64(1 / 3)     # numpy scalars live in real __dict__s
+    G.synthesis.b8.conv1.register_buffer("scratch", torch.zeros(2), persistent=False)
+    assert G.synthesis.b8.conv1._non_persistent_buffers_set
     path = tmp_path / "net.pkl"
-    path.write_bytes(_make_pickle(G, kw))
+    blob = _make_pickle(G, kw, protocol=protocol)
+    if protocol <= 3:
+        assert b"set" in blob
+    path.write_bytes(blob)
     G2 = legacy.load_generator_pkl(str(path), device="cpu")
+    del G.synthesis.b8.conv1.scratch
     a, b = G.state_dict(), G2.state_dict()
     assert a.keys() == b.keys()
     for k in a:
@@ -103,10 +113,13 @@ def test_load_generator_cli_path(tmp_path):
     G, kw = _generator()
     path = tmp_path / "net.pkl"
     path.write_bytes(_make_pickle(G, kw))
-    G2 = load_generator(str(path), 32, "cpu")
+    from stylemc_amd.find_direction import until_k_for
+    # --resolution selects the rendered depth (find_direction.py:263), not the generator: any value loads
+    G2 = load_generator(str(path), 16, "cpu")
     assert torch.equal(G2.synthesis.b32.conv1.weight, G.synthesis.b32.conv1.weight)
+    assert until_k_for(G2, 16) == 2 and until_k_for(G2, 32) == 3
     with pytest.raises(SystemExit):
-        load_generator(str(path), 64, "cpu")
+        until_k_for(G2, 64)
 
 
 class _Evil:

@@ -27,7 +27,7 @@ def main():
     dev = torch.device("cuda", 0)
     G = load_generator("synthetic", 1024, dev)
     styles = synthetic.synthetic_styles(129, seed=0).to(dev)
-    clip = build_clip_losses("small", dev, "a", "b")
+    clip = build_clip_losses("small", dev, "a", "b", synthetic_weights=True)
     f = DirectionFinder(G, styles, clip, IDLoss("a", device=dev, weights=None), resolution=1024, batch_size=4,
                         seed=0, init_delta=initial_delta(0, 0.01), n_epochs=1000,
                         batch_losses=not a.no_batch_losses, overlap=not a.no_overlap)

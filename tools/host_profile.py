@@ -21,7 +21,7 @@ def main():
     dev = torch.device("cuda", 0)
     G = load_generator("synthetic", 1024, dev)
     styles = synthetic.synthetic_styles(129, seed=0).to(dev)
-    f = DirectionFinder(G, styles, build_clip_losses("small", dev, "a", "b"), IDLoss("a", device=dev, weights=None),
+    f = DirectionFinder(G, styles, build_clip_losses("small", dev, "a", "b", synthetic_weights=True), IDLoss("a", device=dev, weights=None),
                         resolution=1024, batch_size=4, seed=0, init_delta=initial_delta(0, 0.01), n_epochs=1000)
     for _ in range(3):
         f.step()

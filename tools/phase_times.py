@@ -46,7 +46,7 @@ def main():
 
     G = FD.load_generator("synthetic", 1024, dev)
     styles = synthetic.synthetic_styles(129, seed=0).to(dev)
-    f = F(G, styles, FD.build_clip_losses("small", dev, "a", "b"), IDLoss("a", device=dev, weights=None),
+    f = F(G, styles, FD.build_clip_losses("small", dev, "a", "b", synthetic_weights=True), IDLoss("a", device=dev, weights=None),
           resolution=1024, batch_size=4, seed=0, init_delta=FD.initial_delta(0, 0.01), n_epochs=1000, synth_fn=synth)
     for _ in range(3):
         f.step()

@@ -11,7 +11,7 @@ from stylemc_amd import synthetic  # noqa: E402
 dev = "cuda"
 text = synthetic.text_direction("a", "b")
 for bs in (2, 4):
-    clip = CLIPLoss(dev, text_features=text, seed=4)
+    clip = CLIPLoss(dev, text_features=text, synthetic_weights=True, seed=4)
     idl = IDLoss(device=dev, weights=None, seed=3)
     for name, fn in [("clip", lambda x: clip.per_sample(torch.nn.functional.interpolate(x.detach(), 224), torch.nn.functional.interpolate(x, 224)).sum()),
                      ("id", lambda x: idl.per_sample(x, x.detach()).sum())]:
