@@ -27,7 +27,8 @@ def _run_pair(res, cbase, n_items, bs, iters, impl="hip"):
     text = synthetic.text_direction("a photo of a face of a feminine woman", "a photo of a face of a man")
     styles = synthetic.synthetic_styles(n_items, seed=5)
     init = initial_delta(0, 0.01)
-    n_epochs = -(-iters // -(-n_items // bs))   # enough epochs for `iters` iterations (same lr schedule both sides)
+    # enough epochs for `iters` iterations, plus one so that the last step's cosine lr is not 0
+    n_epochs = -(-iters // -(-n_items // bs)) + 1
     # CPU oracle
     Go = oracle_generator(res, cbase, seed=0)
     vis = OL.CLIPVisual().eval()
