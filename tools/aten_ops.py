@@ -26,7 +26,7 @@ def main():
         for _ in range(3):
             f.step()
         torch.cuda.synchronize()
-    print(prof.key_averages(group_by_input_shape=True).table(sort_by="count", row_limit=45, max_name_column_width=40,
+    print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_device_time_total", row_limit=60, max_name_column_width=40,
                                                              max_shapes_column_width=60))
 
 
