@@ -488,143 +488,145 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_lds_kernel(GemmParams p) {
     gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32);
 }
 
-// Halo-tile variant for the 32-output-channel 3x3 stride-1 'same' convs (the r = 1024 conv1, forward and data
-// gradient).  With only 32 output channels the tap-major GEMM above re-reads every input pixel once per tap
-// (9x) through L2 for 16 FLOP per LDS byte.  Here a workgroup owns one row segment of BM positions and stages,
-// per CK-channel step, the 3-row halo X[CK][3][BM+2] plus all taps' weight slabs W[9][CK][32]; the nine taps
-// then run out of LDS (27-35 FLOP per staged byte).  Persistent: workgroup g takes tiles g, g + G, ...; the
-// (tile, channel-step) sequence is one 2-stage LDS ring, so the next tile's halo lands during this tile's
-// MFMAs and epilogue.  With G a multiple of 8 a column segment stays on one XCD (tile % 8 == XCD), and the
-// rows that share halo lines run concurrently on the same L2.
-template <int TM, int CK>
-__global__ __launch_bounds__(NT, 2) void conv3_halo_kernel(GemmParams p, int ntiles) {
-    constexpr int BO = 32;
-    constexpr int BM = 4 * TM * 32;                 // positions of one row segment (4 waves x TM blocks)
-    constexpr int HWD = BM + 2;                     // halo row width
-    // floats per channel of the halo, padded to 32 mod 64 so the two half-waves' B reads (channels k, k+1)
-    // fall on disjoint LDS banks
-    constexpr int CH = ((3 * HWD - 32 + 63) / 64) * 64 + 32;
-    constexpr int XF = CK * CH;
-    constexpr int XCH = (XF + 63) / 64;             // 64-float DMA chunks of the halo
-    constexpr int XS = XCH * 64;
-    constexpr int WT = CK * BO;                     // one tap's weight slab
-    static_assert(WT == 256 || WT == 128, "16-B-per-lane weight DMAs cover one or two tap slabs");
-    constexpr int TPD = 256 / WT;                   // tap slabs per weight DMA
-    constexpr int ND = (9 + TPD - 1) / TPD;         // weight DMAs per step
-    constexpr int STAGE = XS + ND * 256;
+// Row-halo variant for the 3x3 stride-1 'same' convs whose position tiles are row segments (W % BM == 0: the
+// r >= 128 conv1 forward and data gradient).  The tap-major kernel above stages one BKT x BM input slab per tap,
+// so every input pixel crosses L2 -> LDS nine times.  Here a K step is (tap row dy, BKT channels): the slab is
+// the input row a + dy over [b0 - 4, b0 + BM + 4) -- one 16-B DMA lane per 4 pixels, aligned because W and b0
+// are multiples of 4 -- and the three taps dx = -1, 0, 1 of that row read it at offsets 3, 4, 5.  Input staging
+// per FLOP drops 3x and the DMA instruction count ~3x; weights for the three taps ride in the same step.
+// Out-of-image pixels (row ends, rows -1 and H) come back as zeros from the buffer range check.
+struct RowTaps {
+    int t[3][3];  // packed-weight tap index of (dy + 1, dx + 1)
+};
+
+template <int WO, int WM, int TO, int TM, int BKT>
+struct RowCfg {
+    static constexpr int BO = WO * TO * 32;
+    static constexpr int BM = WM * TM * 32;
+    static constexpr int CHK = (BM + 8) / 4;               // 16-B chunks of one halo'd row
+    // floats per staged row: the smallest >= CHK * 4 that is 32 mod 64 (the two half-waves' B reads, rows k and
+    // k + 1, fall on disjoint LDS banks)
+    static constexpr int PITCH = ((CHK * 4 - 32 + 63) / 64) * 64 + 32;
+    static constexpr int XL = BKT * PITCH / 4;               // DMA lanes of the X slab (pitch padding included)
+    static constexpr int XJ = (XL + 63) / 64;                // X DMA wave-instructions per step
+    static constexpr int XF = XJ * 64 * 4;                   // floats reserved for X (whole instructions)
+    static constexpr int WF = 3 * BKT * BO;                  // floats of the three taps' weight slabs
+    static constexpr int WJ = WF / 256;                      // weight DMA wave-instructions per step (16 B/lane)
+    static constexpr int STAGE = XF + WF;
+    static_assert(WF % 256 == 0, "weight slabs split into whole 1-KB DMAs");
+    static_assert(PITCH % 64 == 32 && PITCH >= CHK * 4, "row pitch");
+};
+
+template <int WO, int WM, int TO, int TM, int BKT>
+__global__ __launch_bounds__(NT, 2) void conv_row_kernel(GemmParams p, RowTaps rt) {
+    using C = RowCfg<WO, WM, TO, TM, BKT>;
+    constexpr int BO = C::BO, BM = C::BM, PITCH = C::PITCH, STAGE = C::STAGE;
+    constexpr int RCH = PITCH / 4;                           // DMA lanes per staged row
+    static_assert(WO * WM == 4, "4 waves");
     __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave;
+    const int wo = wave / WM, wm = wave % WM;
     const PhaseDev& ph = p.ph[0];
-    const int H = p.in_h, W = p.in_w;
-    const int hw = H * W;
-    const int tpr = W / BM;                         // tiles per row
-    const int kpt = p.cin / CK;                     // channel steps per tile
-    const int G = gridDim.x;
-    const int nmine = (int)blockIdx.x < ntiles ? (ntiles - (int)blockIdx.x + G - 1) / G : 0;
-    const int S = nmine * kpt;
+    const int H = p.in_h, W = p.in_w, hw = H * W;
+    int tm = blockIdx.x, tn = blockIdx.y;
+    if (p.ntn) {  // XCD-aware bijective tile order (see conv_gemm_lds_kernel)
+        const int nwg = gridDim.x, orig = blockIdx.x;
+        const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+        const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+        tm = wgid / p.ntn;
+        tn = wgid - tm * p.ntn;
+    }
+    const int m0 = tm * BM;
+    if (m0 >= p.n * hw) return;
+    const int nn = m0 / hw;
+    const int rem = m0 - nn * hw;
+    const int a = rem / W, b0 = rem - a * W;
+    const int o0 = tn * BO;
+    const int cpk = p.cin / BKT;
+    const int ks_total = 3 * cpk;
     const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * hw * 4), 0x00020000);
-    int toff[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) toff[t] = (ph.dy[t] + 1) * HWD + (ph.dx[t] + 1);
+    const float* wk = ph.wk + (ph.wstride ? (int64_t)nn * ph.wstride : 0);
 
-    auto decode = [&](int ti, int& n, int& a, int& b0) {
-        int t = (int)blockIdx.x + ti * G;
-        const int bs = t % tpr;
-        t /= tpr;
-        a = t % H;
-        n = t / H;
-        b0 = bs * BM;
-    };
-    auto issue = [&](int s) {
-        const int ti = s / kpt;
-        const int ci0 = (s - ti * kpt) * CK;
-        int n, a, b0;
-        decode(ti, n, a, b0);
-        float* xs = smem + (s & 1) * STAGE;
-        const int cbase = n * p.cin + ci0;
-        // halo chunk -> per-lane source offset; branch-free (out-of-range lanes read 0 via the buffer bound)
-        auto halo_dma = [&](int chunk) {
-            const int f = chunk * 64 + lane;
-            const int ch = f / CH;
-            const int rem = f - ch * CH;
-            const int r = rem / HWD;
-            const int c = rem - r * HWD;
-            const int iy = a + r - 1, ix = b0 + c - 1;
-            const bool ok = f < XF && r < 3 && iy >= 0 && iy < H && ix >= 0 && ix < W;
-            const int v = (((cbase + ch) * H + iy) * W + ix) * 4;
+    auto issue = [&](int ks, int slot) {
+        const int dyi = ks / cpk;
+        const int ci0 = (ks - dyi * cpk) * BKT;
+        const int iy = a + dyi - 1;
+        const bool rowok = iy >= 0 && iy < H;
+        float* xs = smem + slot * STAGE;
+        // X slab: lane L -> (row L / RCH, 16-B chunk L % RCH) at pixel b0 - 4 + 4 * chunk
+#pragma unroll
+        for (int j = wave; j < C::XJ; j += 4) {
+            const int L = j * 64 + lane;
+            const int row = L / RCH, ch = L - row * RCH;
+            const int x = b0 - 4 + 4 * ch;
+            const bool ok = rowok && row < BKT && ch < C::CHK && x >= 0 && x < W;
+            const int v = ((((nn * p.cin + ci0 + row) * H + iy) * W) + x) * 4;
             const int msk = -(int)ok;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (__attribute__((address_space(3))) void*)(xs + chunk * 64),
-                                                     4, (v & msk) | (0x7ffffff0 & ~msk), 0, 0, 0);
-        };
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (__attribute__((address_space(3))) void*)(xs + j * 256), 16,
+                                                     (v & msk) | (0x7ffffff0 & ~msk), 0, 0, 0);
+        }
+        // weights of the three taps of row dy: [tt][ci][o] slabs, 4 floats per lane
+        float* ws = xs + C::XF;
 #pragma unroll
-        for (int j = 0; j < XCH / 4; ++j) halo_dma(wave + 4 * j);
-        if (wave < XCH % 4) halo_dma(4 * (XCH / 4) + wave);
-        const float* wb = ph.wk + (ph.wstride ? (int64_t)n * ph.wstride : 0) + (int64_t)ci0 * BO +
-                          (lane % (64 / TPD)) * 4;
-        auto w_dma = [&](int d) {
-            const int t = std::min(d * TPD + lane / (64 / TPD), 8);  // a tenth slab (TPD 2) re-reads tap 8 into padding
-            __builtin_amdgcn_global_load_lds((const void*)(wb + (int64_t)t * p.cin * BO),
-                                             (__attribute__((address_space(3))) void*)(xs + XS + d * 256), 16, 0, 0);
-        };
-#pragma unroll
-        for (int j = 0; j < ND / 4; ++j) w_dma(wave + 4 * j);
-        if (wave < ND % 4) w_dma(4 * (ND / 4) + wave);
+        for (int j = wave; j < C::WJ; j += 4) {
+            const int f = (j * 64 + lane) * 4;
+            const int tt = f / (BKT * BO);
+            const int r2 = f - tt * (BKT * BO);
+            const int ci = r2 / BO, o = r2 - ci * BO;
+            const float* src = wk + ((int64_t)rt.t[dyi][tt] * p.cin + ci0 + ci) * p.cout + o0 + o;
+            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(ws + j * 256),
+                                             16, 0, 0);
+        }
     };
 
-    f32x16 acc[1][TM];
+    f32x16 acc[TO][TM];
 #pragma unroll
-    for (int j = 0; j < TM; ++j)
+    for (int i = 0; i < TO; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.f;
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
     const int kh = lane >> 5, l32 = lane & 31;
-    if (S > 0) issue(0);
-    for (int s = 0; s < S; ++s) {
+    if (ks_total > 0) issue(0, 0);
+    for (int ks = 0; ks < ks_total; ++ks) {
         wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();  // step s landed for every wave; slot (s+1)&1 is no longer read
+        __builtin_amdgcn_s_barrier();  // step ks landed for every wave; the other slot is free
         asm volatile("" ::: "memory");
-        const float* Xs = smem + (s & 1) * STAGE + kh * CH + wm * TM * 32 + l32;
-        const float* Ws = smem + (s & 1) * STAGE + XS + kh * BO + l32;
-        // fragments of tap t+1 are read under tap t's MFMAs; the next step's DMAs go out after tap 0's
-        float af[2][CK / 2], bf[2][CK / 2][TM];
-        auto frag = [&](int t, int b) {
+        const int slot = ks & 1;
+        const float* Xs = smem + slot * STAGE + kh * PITCH + 3 + wm * TM * 32 + l32;
+        const float* Ws = smem + slot * STAGE + C::XF + kh * BO + wo * TO * 32 + l32;
 #pragma unroll
-            for (int q = 0; q < CK / 2; ++q) {
-                af[b][q] = Ws[t * WT + 2 * q * BO];
+        for (int tt = 0; tt < 3; ++tt) {
 #pragma unroll
-                for (int j = 0; j < TM; ++j) bf[b][q][j] = Xs[toff[t] + 2 * q * CH + j * 32];
+            for (int k0 = 0; k0 < BKT; k0 += 8) {
+                float af[4][TO], bf[4][TM];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                    for (int i = 0; i < TO; ++i) af[q][i] = Ws[(tt * BKT + k0 + 2 * q) * BO + i * 32];
+#pragma unroll
+                    for (int j = 0; j < TM; ++j) bf[q][j] = Xs[(k0 + 2 * q) * PITCH + tt + j * 32];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int i = 0; i < TO; ++i)
+#pragma unroll
+                        for (int j = 0; j < TM; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q][i], bf[q][j], acc[i][j], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (tt == 0 && k0 == 0 && ks + 1 < ks_total) issue(ks + 1, slot ^ 1);
             }
-        };
-        frag(0, 0);
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            if (t + 1 < 9) frag(t + 1, (t + 1) & 1);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < CK / 2; ++q)
-#pragma unroll
-                for (int j = 0; j < TM; ++j)
-                    acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t & 1][q], bf[t & 1][q][j], acc[0][j], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (t == 0 && s + 1 < S) issue(s + 1);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const int ti = s / kpt;
-        if (s - ti * kpt == kpt - 1) {
-            int n, a, b0;
-            decode(ti, n, a, b0);
-            const int m0 = n * hw + a * W + b0;
-            gemm_epilogue<1, 4, 1, TM>(p, ph, acc, m0, 0, p.n * hw, hw, 0, 0, wm, kh, l32);
-#pragma unroll
-            for (int j = 0; j < TM; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.f;
-        }
     }
+    gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, p.n * hw, hw, 0, wo, wm, kh, l32);
 }
 
 // Style-scaled input for the low-resolution layers: out[n][i][p] = x[n][i][p] * s[n][i] (float4 when hw % 4 == 0).
@@ -871,10 +873,9 @@ bool convt_fusable(int cin, int cout, int in_h, int in_w, int y_h, int y_w, cons
                    const smc_conv_epilogue* epi, ConvTParams* q) {
     if (nph != 4 || y_h != 2 * in_h + 1 || y_w != 2 * in_w + 1) return false;
     if (epi && (epi->mode != SMC_EPI_STORE || epi->residual)) return false;
-    if (getenv("SMC_NO_CONVT_FUSION")) return false;
     // measured (tools/bench_gemm.py): the fused kernel (1 wave/SIMD, 128 accumulators) wins only on the
     // 32-channel 1024-px layer (51 vs 42 TF/s); the per-phase kernel is faster on every wider layer.
-    if (cout > 32 && !getenv("SMC_FORCE_CONVT_FUSION")) return false;
+    if (cout > 32) return false;
     ConvTParams t{};
     int count = 0;
     for (int k = 0; k < 4; ++k) {
@@ -908,10 +909,8 @@ ConvTCfg convt_cfg(int cout) {
     if (cout % 128 == 0) return {128, 64, 0};
     if (cout % 64 == 0) return {64, 128, 1};
     // 32 x 128 tile: 159 VGPR + 80 AGPR -> 2 workgroups per CU (the 32 x 256 tile's 256 + 160 allow one):
-    // 763 -> 620 us on the r = 1024 conv0 (tools/bench_gemm.py).  SMC_CONVT_BM=256 restores the wide tile.
-    static const int bm = getenv("SMC_CONVT_BM") ? atoi(getenv("SMC_CONVT_BM")) : 128;
-    if (bm == 128) return {32, 128, 3};
-    return {32, 256, 2};
+    // 763 -> 620 us on the r = 1024 conv0 (tools/bench_gemm.py)
+    return {32, 128, 3};
 }
 
 int plan_split_convt(int n, int cin, int cout, int in_h, int in_w) {
@@ -919,10 +918,6 @@ int plan_split_convt(int n, int cin, int cout, int in_h, int in_w) {
     const int64_t M = (int64_t)n * (in_h + 1) * (in_w + 1);
     const int64_t blocks = smc::ceil_div(M, c.bm) * smc::ceil_div(cout, c.bo);
     const int ks = 4 * (cin / BK);
-    if (const char* f = getenv("SMC_FORCE_SPLIT")) {
-        int v = atoi(f);
-        if (v >= 1) return v < ks ? v : ks;
-    }
     const int64_t target = 2LL * smc::device_cu_count();
     if (blocks >= target) return 1;
     int s = (int)smc::ceil_div(target, blocks > 0 ? blocks : 1);
@@ -939,19 +934,10 @@ struct Cfg {
 int pick_cfg(int cout, Cfg* c) {
     // 32/64-channel layers: 128-position tiles (twice the workgroups of the 256-position ones, half the LDS
     // per workgroup): r = 512 conv0 451 -> 424 us, r = 1024 bwd conv0 426 -> 396 us, the rest within 1 %
-    // (tools/bench_gemm.py).  SMC_NARROW_BM=256 restores the wide tiles.
-    static const bool narrow128 = !(getenv("SMC_NARROW_BM") && atoi(getenv("SMC_NARROW_BM")) == 256);
+    // (tools/bench_gemm.py)
     if (cout % 128 == 0) { *c = {128, 128}; return 0; }
-    if (cout % 64 == 0) {
-        if (narrow128) { *c = {64, 128}; return 5; }
-        *c = {64, 256};
-        return 1;
-    }
-    if (cout % 32 == 0 || cout == 16) {  // cout 16: half-empty tile, masked
-        if (narrow128) { *c = {32, 128}; return 4; }
-        *c = {32, 256};
-        return 2;
-    }
+    if (cout % 64 == 0) { *c = {64, 128}; return 5; }
+    if (cout % 32 == 0 || cout == 16) { *c = {32, 128}; return 4; }  // cout 16: half-empty tile, masked
     return -1;
 }
 
@@ -964,10 +950,6 @@ int plan_split(int n, int cin, int cout, const smc_conv_phase* ph, int nph, cons
         blocks += smc::ceil_div(M, c.bm) * smc::ceil_div(cout, c.bo);
         const int ks = ph[i].ntaps * (cin / BK);
         if (ks < min_ks) min_ks = ks;
-    }
-    if (const char* f = getenv("SMC_FORCE_SPLIT")) {
-        int v = atoi(f);
-        if (v >= 1) return v < min_ks ? v : min_ks;
     }
     const int64_t target = 2LL * smc::device_cu_count();
     if (blocks >= target) return 1;
@@ -982,27 +964,31 @@ int plan_split(int n, int cin, int cout, const smc_conv_phase* ph, int nph, cons
 // workgroups that never straddle two images.  `scaled_ok` reports the latter.
 bool lds_shape_ok(int n, int cin, int cout, int in_h, int in_w, const smc_conv_phase* ph, int nph, const Cfg& c,
                   bool* scaled_ok) {
-    static const bool off = getenv("SMC_NO_LDS_DMA") != nullptr;  // A/B knob (tools/bench_gemm.py)
     bool so = true;
     for (int i = 0; i < nph; ++i) so = so && ((int64_t)ph[i].out_h * ph[i].out_w) % c.bm == 0;
     if (scaled_ok) *scaled_ok = so;
-    return !off && cout % c.bo == 0 && cin % BK == 0 && (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31);
+    return cout % c.bo == 0 && cin % BK == 0 && (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31);
 }
 
-// conv3_halo_kernel<1, 8> shapes: one 9-tap phase with |dy|, |dx| <= 1 that maps the input grid onto an
-// equal output grid (3x3 stride-1 'same'), 32 output channels, cin % 8 == 0, rows of whole 128-position
-// segments.  Opt-in (SMC_HALO=1): measured slower than the tap-major LDS-DMA kernel on the r = 1024 conv1
-// (962 vs 822 us), kept as the A/B baseline for the next attempt.
-bool halo_ok(int n, int cin, int cout, int in_h, int in_w, int y_h, int y_w, const smc_conv_phase* ph, int nph) {
-    static const bool on = getenv("SMC_HALO") && atoi(getenv("SMC_HALO")) != 0;
-    if (!on || nph != 1 || cout != 32 || cin % 8 != 0 || in_w % 128 != 0) return false;
+// conv_row_kernel shapes: one 9-tap phase covering {-1,0,1}^2 that maps the input grid onto an equal output
+// grid (3x3 stride-1 'same'), rows of whole BM-position segments, cin % 16 == 0, cout a multiple of the tile.
+bool row_ok(int n, int cin, int cout, int in_h, int in_w, int y_h, int y_w, const smc_conv_phase* ph, int nph,
+            const Cfg& c, RowTaps* rt) {
+    if (nph != 1 || cin % 16 != 0 || cout % c.bo != 0 || in_w % c.bm != 0 || in_w % 4 != 0) return false;
     const smc_conv_phase& q = ph[0];
     if (q.ntaps != 9 || q.in_stride != 1 || q.out_h != in_h || q.out_w != in_w || y_h != in_h || y_w != in_w ||
         q.out_oy != 0 || q.out_ox != 0 || q.out_sy != 1 || q.out_sx != 1)
         return false;
-    for (int t = 0; t < 9; ++t)
-        if (q.tap_dy[t] < -1 || q.tap_dy[t] > 1 || q.tap_dx[t] < -1 || q.tap_dx[t] > 1) return false;
-    return (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31);
+    int seen = 0;
+    for (int t = 0; t < 9; ++t) {
+        const int dy = q.tap_dy[t], dx = q.tap_dx[t];
+        if (dy < -1 || dy > 1 || dx < -1 || dx > 1) return false;
+        const int bit = 1 << ((dy + 1) * 3 + dx + 1);
+        if (seen & bit) return false;
+        seen |= bit;
+        if (rt) rt->t[dy + 1][dx + 1] = t;
+    }
+    return seen == 511 && (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31);
 }
 
 // floats of per-sample weights (n x sum_p taps_p * cin * cout), 64-float aligned
@@ -1012,38 +998,18 @@ int64_t wsample_floats(int n, int cin, int cout, const smc_conv_phase* ph, int n
     return ((t * n + 63) / 64) * 64;
 }
 
-// LDS ring depth per tile config (measured on MI355X, tools/bench_gemm.py, FFHQ-1024 shapes, batch 4):
-// two stages (32-41 KB of LDS -> 3-4 workgroups per CU) beat three or four on every layer: the
-// occupancy hides the DMA latency better than a deeper ring (total 12.6 vs 13.0 / 13.3 ms, register-
-// staged kernel 13.2 ms).  SMC_LDS_STAGES (wide 128x128 tile) / SMC_LDS_NARROW (32/64 x 256 tiles)
-// override the depth (2..4; 0 = register-staged kernel) for A/B runs.
-int lds_stages(int cfg) {
-    auto knob = [](const char* name) {
-        const char* f = getenv(name);
-        const int s = f ? atoi(f) : 2;
-        return s <= 0 ? 0 : (s < 2 ? 2 : (s > 4 ? 4 : s));
-    };
-    static const int wide = knob("SMC_LDS_STAGES");
-    static const int narrow = knob("SMC_LDS_NARROW");
-    return cfg == 0 ? wide : narrow;
-}
-
-// BK = 32 for the wide tile on the long-K 512-channel layers (SMC_LDS_BK32=0 disables)
-bool lds_bk32(int cfg, int cin) {
-    static const bool on = [] {
-        const char* f = getenv("SMC_LDS_BK32");
-        return !f || atoi(f) != 0;
-    }();
-    return on && cfg == 0 && cin % 32 == 0 && cin >= 512;
-}
+// LDS ring depth: two stages (32-41 KB of LDS -> 3-4 workgroups per CU) beat three or four on every layer
+// (measured on MI355X, tools/bench_gemm.py, FFHQ-1024 shapes, batch 4): the occupancy hides the DMA latency
+// better than a deeper ring (total 12.6 vs 13.0 / 13.3 ms, register-staged kernel 13.2 ms).
+// BK = 32 for the wide tile on the long-K 512-channel layers.
+bool lds_bk32(int cfg, int cin) { return cfg == 0 && cin % 32 == 0 && cin >= 512; }
 
 // 64x64 tile (4 waves of one 32x32 block each) for GEMMs whose cout-based tile leaves most CUs idle (the
 // IR-SE50 7..28-px stages, the synthesis 4..32-px blocks): 4x the workgroups before any split-K, so fewer
 // and shorter partial planes.  LDS-DMA kernel only; SMC_NO_SMALL_TILE=1 disables (A/B knob).
 bool small_tile_ok(int n, int cin, int cout, int in_h, int in_w, const smc_conv_phase* ph, int nph, bool has_s,
                    const Cfg& base) {
-    static const bool off = getenv("SMC_NO_SMALL_TILE") != nullptr;
-    if (off || cout % 64 != 0 || lds_stages(1) == 0) return false;
+    if (cout % 64 != 0) return false;
     int64_t blocks = 0;
     int taps_all = 0;
     for (int i = 0; i < nph; ++i) {
@@ -1053,11 +1019,7 @@ bool small_tile_ok(int n, int cin, int cout, int in_h, int in_w, const smc_conv_
     // threshold measured on the FFHQ-1024 / IR-SE50 shapes (tools/bench_gemm.py, tools/prof_irse.py): the
     // 128x128 tile with split-K stays ahead from 128 tiles up (r = 32 conv1); below that the 64x64 tile wins on
     // the sum (synthesis GEMMs 12.14 ms at 128 vs 12.30 at 256; IR-SE50 pair 4.85 vs 5.06 ms at 32)
-    static const int64_t max_blocks = [] {
-        const char* f = getenv("SMC_SMALL_TILE_MAX_BLOCKS");
-        return f ? (int64_t)atoll(f) : (int64_t)128;
-    }();
-    if (blocks >= max_blocks) return false;
+    if (blocks >= 128) return false;
     const Cfg sm{64, 64};
     bool scaled_ok = false;
     if (!lds_shape_ok(n, cin, cout, in_h, in_w, ph, nph, sm, &scaled_ok)) return false;
@@ -1144,9 +1106,8 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     int cfg = pick_cfg(cout, &c);
     ConvTParams ctp{};
     const bool fused_t = convt_fusable(cin, cout, in_h, in_w, y_h, y_w, phases, nphases, epi, &ctp);
-    static const bool no_pre = getenv("SMC_NO_PRESCALE") != nullptr;  // A/B knob
     const int64_t pre_fl = prescale_floats(n, cin, cout, phases, nphases);
-    const bool prescale = s_in && !fused_t && !no_pre && pre_fl > 0 && (int64_t)n * cin * in_h * in_w <= pre_fl &&
+    const bool prescale = s_in && !fused_t && pre_fl > 0 && (int64_t)n * cin * in_h * in_w <= pre_fl &&
                           (in_h * in_w) % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     const float* s_prescale = s_in;
     if (prescale) s_in = nullptr;  // the GEMM reads x * s from the workspace with the shared weights
@@ -1225,15 +1186,13 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     }
     dim3 grid((unsigned)smc::ceil_div(max_m, c.bm), (unsigned)smc::ceil_div(cout, c.bo), (unsigned)(nphases * nsplit));
     bool scaled_ok = false;
-    const int nst = lds_stages(cfg);
     // per-sample tiling pays where the per-sample weights are small next to the input planes (the
     // high-resolution conv0 layers); on the 512-channel low-resolution layers writing n weight copies
     // costs more than the register-staged kernel's in-loop scaling (tools/bench_gemm.py)
     int taps_all = 0;
     for (int i = 0; i < nphases; ++i) taps_all += phases[i].ntaps;
     const bool small_w = (int64_t)taps_all * cout <= (int64_t)in_h * in_w;
-    if (nst && lds_shape_ok(n, cin, cout, in_h, in_w, phases, nphases, c, &scaled_ok) &&
-        (!s_in || scaled_ok || small_w)) {
+    if (lds_shape_ok(n, cin, cout, in_h, in_w, phases, nphases, c, &scaled_ok) && (!s_in || scaled_ok || small_w)) {
         if (s_in && !scaled_ok) {
             // per-sample tiling: grid.x = n x (tiles of the largest phase image)
             int64_t tps = 0;
@@ -1263,57 +1222,41 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             if (rc != SMC_OK) return rc;
         }
         p.s = nullptr;
-        if (nsplit == 1 && halo_ok(n, cin, cout, in_h, in_w, y_h, y_w, phases, nphases)) {
-            static const int wpc = [] {
-                const char* f = getenv("SMC_HALO_WPC");
-                return f && atoi(f) > 0 ? atoi(f) : 3;
-            }();
-            static const int tm = getenv("SMC_HALO_TM") && atoi(getenv("SMC_HALO_TM")) == 2 ? 2 : 1;  // A/B knobs
-            static const int ck = getenv("SMC_HALO_CK") && atoi(getenv("SMC_HALO_CK")) == 4 ? 4 : 8;
-            const int bm = tm == 2 && in_w % 256 == 0 ? 256 : 128;
-            const int ntiles = n * in_h * (in_w / bm);
-            const int g = std::min(ntiles, smc::device_cu_count() * (bm == 256 ? 2 : wpc));
-            if (bm == 256) hipLaunchKernelGGL((conv3_halo_kernel<2, 8>), dim3((unsigned)g), dim3(NT), 0, st, p, ntiles);
-            else if (ck == 4)
-                hipLaunchKernelGGL((conv3_halo_kernel<1, 4>), dim3((unsigned)std::min(ntiles, smc::device_cu_count() * 4)),
-                                   dim3(NT), 0, st, p, ntiles);
-            else hipLaunchKernelGGL((conv3_halo_kernel<1, 8>), dim3((unsigned)g), dim3(NT), 0, st, p, ntiles);
-            return smc::check_launch("smc_conv_gemm_f32 (halo tile)");
-        }
-        static const bool no_swz = getenv("SMC_NO_XCD_SWIZZLE") != nullptr;  // A/B knob
-        if (!no_swz) {
-            p.ntn = (int)grid.y;
-            grid.x *= grid.y;
-            grid.y = 1;
+        // XCD-aware tile order: one grid dimension, column tiles fastest (see conv_gemm_lds_kernel)
+        p.ntn = (int)grid.y;
+        grid.x *= grid.y;
+        grid.y = 1;
+        RowTaps rt{};
+        if (nsplit == 1 && !p.per_sample && row_ok(n, cin, cout, in_h, in_w, y_h, y_w, phases, nphases, c, &rt)) {
+            if (cfg == 0) hipLaunchKernelGGL((conv_row_kernel<2, 2, 2, 2, 16>), grid, dim3(NT), 0, st, p, rt);
+            else if (cfg == 5) hipLaunchKernelGGL((conv_row_kernel<2, 2, 1, 2, 16>), grid, dim3(NT), 0, st, p, rt);
+            else hipLaunchKernelGGL((conv_row_kernel<1, 4, 1, 1, 16>), grid, dim3(NT), 0, st, p, rt);
+            return smc::check_launch("smc_conv_gemm_f32 (row-halo)");
         }
 #define SMC_LAUNCH_LDS(WO_, WM_, TO_, TM_)                                                                          \
     do {                                                                                                          \
-        if (nst == 2 && tag) hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 2, 1>), grid, dim3(NT), 0, st, p); \
-        else if (nst == 2) hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 2>), grid, dim3(NT), 0, st, p); \
-        else if (nst == 3) hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 3>), grid, dim3(NT), 0, st, p); \
-        else hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 4>), grid, dim3(NT), 0, st, p);     \
+        if (tag) hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 2, 1>), grid, dim3(NT), 0, st, p); \
+        else hipLaunchKernelGGL((conv_gemm_lds_kernel<WO_, WM_, TO_, TM_, 16, 2>), grid, dim3(NT), 0, st, p);       \
     } while (0)
-        if (cfg == 0 && lds_bk32(cfg, cin) && nst == 2 && tag)
+        if (cfg == 0 && lds_bk32(cfg, cin) && tag)
             hipLaunchKernelGGL((conv_gemm_lds_kernel<2, 2, 2, 2, 32, 2, 1>), grid, dim3(NT), 0, st, p);
-        else if (cfg == 0 && lds_bk32(cfg, cin) && nst == 2)
+        else if (cfg == 0 && lds_bk32(cfg, cin))
             hipLaunchKernelGGL((conv_gemm_lds_kernel<2, 2, 2, 2, 32, 2>), grid, dim3(NT), 0, st, p);
         else if (cfg == 0) SMC_LAUNCH_LDS(2, 2, 2, 2);
-        else if (cfg == 1) SMC_LAUNCH_LDS(1, 4, 2, 2);
         else if (cfg == 3) SMC_LAUNCH_LDS(2, 2, 1, 1);
         else if (cfg == 4) SMC_LAUNCH_LDS(1, 4, 1, 1);
-        else if (cfg == 5) SMC_LAUNCH_LDS(2, 2, 1, 2);
-        else SMC_LAUNCH_LDS(1, 4, 1, 2);
+        else SMC_LAUNCH_LDS(2, 2, 1, 2);
 #undef SMC_LAUNCH_LDS
         rc = smc::check_launch("smc_conv_gemm_f32 (LDS-DMA)");
         if (rc != SMC_OK || nsplit == 1) return rc;
         return smc_modconv_epilogue_f32(workspace, nsplit, plane_elems, y, n, cout, y_h, y_w, &e, stream);
     }
-    // BK=32 halves the barriers per FLOP; it pays on the long-K 512-channel layers, BK=16 (more
-    // workgroups per CU: 32-40 KB LDS vs 64-80 KB) on the high-resolution ones (tools/bench_gemm.py).
-    bool k32 = cin % 32 == 0 && cin >= 512;
-    if (const char* f = getenv("SMC_FORCE_BK")) k32 = k32 && atoi(f) != 16;  // A/B knob (tools/bench_gemm.py)
-    // raw buffer loads need the input to fit a 32-bit byte offset
-    const bool buf = (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31) && !getenv("SMC_NO_BUFFER_LOADS");
+    // Register-staged kernel: the shapes the LDS-DMA kernel does not take (inputs of 2 GiB or more, style-scaled
+    // inputs whose tiles straddle images with large per-sample weights).  BK = 32 halves the barriers per FLOP; it
+    // pays on the long-K 512-channel layers, BK = 16 (more workgroups per CU: 32-40 KB LDS vs 64-80 KB) on the
+    // high-resolution ones (tools/bench_gemm.py).  Raw buffer loads need the input to fit a 32-bit byte offset.
+    const bool k32 = cin % 32 == 0 && cin >= 512;
+    const bool buf = (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31);
 #define SMC_LAUNCH(WO_, WM_, TO_, TM_)                                                                       \
     do {                                                                                                   \
         if (k32 && buf && tag) hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 32, true, 1>), grid, dim3(NT), 0, st, p); \
@@ -1324,10 +1267,9 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         else hipLaunchKernelGGL((conv_gemm_kernel<WO_, WM_, TO_, TM_, 16, false>), grid, dim3(NT), 0, st, p);             \
     } while (0)
     if (cfg == 0) SMC_LAUNCH(2, 2, 2, 2);
-    else if (cfg == 1) SMC_LAUNCH(1, 4, 2, 2);
     else if (cfg == 4) SMC_LAUNCH(1, 4, 1, 1);
     else if (cfg == 5) SMC_LAUNCH(2, 2, 1, 2);
-    else SMC_LAUNCH(1, 4, 1, 2);
+    else SMC_LAUNCH(2, 2, 1, 1);
 #undef SMC_LAUNCH
     rc = smc::check_launch("smc_conv_gemm_f32");
     if (rc != SMC_OK || nsplit == 1) return rc;

@@ -353,8 +353,7 @@ __global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, 
 }
 
 bool lin_v2_ok(int N, int K, int lda, int ldb) {
-    static const bool off = getenv("SMC_LIN_V1") != nullptr;  // A/B knob (tools/bench_linear.py)
-    return !off && K % L2K == 0 && N % L2N == 0 && lda % 4 == 0 && ldb % 4 == 0;
+    return K % L2K == 0 && N % L2N == 0 && lda % 4 == 0 && ldb % 4 == 0;
 }
 
 int lin_nsplit2(int M, int N, int K) {
@@ -975,15 +974,9 @@ int vit_validate(const smc_vit_config* cfg, int B) {
 
 smc_linear_epilogue epi_none() { return smc_linear_epilogue{}; }
 
-// Split-K partials are reduced by a separate epilogue kernel by default: measured on MI355X (B=4
-// ViT-B/32, tools/bench_vit.py) the in-launch hand-off's per-workgroup L2 write-back of the freshly
-// written slabs costs more than the extra launch (fwd 3.06 vs 1.77 ms).  SMC_VIT_SPLITK_INLAUNCH=1
-// selects the in-launch form (A/B knob).
-bool split_kernel_reduce() {
-    static const bool v = getenv("SMC_VIT_SPLITK_INLAUNCH") == nullptr;
-    return v;
-}
-
+// Split-K partials are reduced by a separate epilogue kernel: measured on MI355X (B=4 ViT-B/32,
+// tools/bench_vit.py) the in-launch hand-off's per-workgroup L2 write-back of the freshly written slabs costs
+// more than the extra launch (fwd 3.06 vs 1.77 ms).
 }  // namespace
 
 // =================================================================================== C ABI: primitives
@@ -1100,7 +1093,7 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
             return SMC_ERR_INVALID;
         }
         return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st,
-                          split_kernel_reduce() ? nullptr : ctr);
+                          nullptr);
     };
     if (hipMemsetAsync(ws.counters, 0, sizeof(int) * (size_t)ws.counter_ints, st) != hipSuccess) {
         smc::set_error("smc_vit: counter memset failed");
@@ -1191,7 +1184,7 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
             return SMC_ERR_INVALID;
         }
         return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st,
-                          split_kernel_reduce() ? nullptr : ctr);
+                          nullptr);
     };
     if (hipMemsetAsync(ws.counters, 0, sizeof(int) * (size_t)ws.counter_ints, st) != hipSuccess) {
         smc::set_error("smc_vit: counter memset failed");

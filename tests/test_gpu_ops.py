@@ -197,30 +197,59 @@ def test_synthesis_layer_grad_subsets():
     close(dxc, dxa, 1e-6, "dx only")
 
 
-@pytest.mark.parametrize("n,cin,r", [(2, 32, 256), (4, 64, 128), (1, 32, 1024)])
-def test_conv_gemm_32ch_vs_conv2d(n, cin, r):
-    """The 32-output-channel 3x3 'same' convs (the r = 1024 conv1 class): forward (per-sample style-scaled
-    weights) and the data gradient (shared flipped weights) against an fp64 CPU convolution (no activation,
-    so no kinks: tolerance 2e-5 of the max).  Under SMC_HALO=1 (tools/halo_ab.sh) the same shapes run
-    conv3_halo_kernel."""
+@pytest.mark.parametrize("n,cin,cout,r", [(2, 32, 32, 256), (4, 64, 32, 128), (1, 32, 32, 1024), (2, 64, 64, 128),
+                                           (1, 48, 64, 256), (1, 128, 128, 128), (1, 256, 256, 128), (2, 512, 512, 16)])
+def test_conv_gemm_same3x3_vs_conv2d(n, cin, cout, r):
+    """3x3 'same' convs (conv1 forward with per-sample style-scaled weights, and its data gradient with the
+    shared flipped weights) against an fp64 CPU convolution (no activation, so no kinks: tolerance 2e-5 of the
+    max).  W >= 128 runs the row-halo kernel (conv_row_kernel) for every tile width (32 / 64 / 128 output
+    channels); W = 16 the tap-major LDS-DMA kernel."""
     import torch.nn.functional as F
     from stylemc_amd import _hip, modconv
     gen = torch.Generator().manual_seed(11)
-    W = torch.randn(32, cin, 3, 3, generator=gen)
+    W = torch.randn(cout, cin, 3, 3, generator=gen)
     P = modconv.PackedConv(W.to(DEV), 1)
     x = torch.randn(n, cin, r, r, generator=gen)
     s = torch.randn(n, cin, generator=gen) * 0.5 + 1
     ph, nph, _, _ = P.fwd_phases(r, r)
-    y = torch.empty(n, 32, r, r, device=DEV)
-    modconv.gemm(x.to(DEV), y, ph, nph, cin, 32, s=s.to(DEV), epi=modconv._epilogue(_hip.EPI_STORE))
+    y = torch.empty(n, cout, r, r, device=DEV)
+    modconv.gemm(x.to(DEV), y, ph, nph, cin, cout, s=s.to(DEV), epi=modconv._epilogue(_hip.EPI_STORE))
     ref = F.conv2d((x * s[:, :, None, None]).double(), W.double(), padding=1)
-    close(y, ref, 2e-5, "halo fwd")
-    g = torch.randn(n, 32, r, r, generator=gen)
+    close(y, ref, 2e-5, "fwd")
+    g = torch.randn(n, cout, r, r, generator=gen)
     phb, nphb = P.bwd_phases(r, r)
     dx = torch.empty(n, cin, r, r, device=DEV)
-    modconv.gemm(g.to(DEV), dx, phb, nphb, 32, cin, epi=modconv._epilogue(_hip.EPI_STORE))
+    modconv.gemm(g.to(DEV), dx, phb, nphb, cout, cin, epi=modconv._epilogue(_hip.EPI_STORE))
     refb = F.conv_transpose2d(g.double(), W.double(), padding=1)
-    close(dx, refb, 2e-5, "halo data grad")
+    close(dx, refb, 2e-5, "data grad")
+
+
+def test_conv_gemm_2gib_input_fallback():
+    """An input of >= 2 GiB (batch 16 of the r = 1024 conv1: 2.1 GB) exceeds the 32-bit buffer offsets of the
+    LDS-DMA / row-halo kernels and runs the register-staged kernel with 64-bit addressing: it must equal the
+    same conv computed in two halves of the batch (each < 2 GiB, the fast kernels), to fp32 summation order."""
+    from stylemc_amd import _hip, modconv
+    gen = torch.Generator().manual_seed(12)
+    n, cin, cout, r = 16, 32, 32, 1024
+    assert n * cin * r * r * 4 >= 2 ** 31
+    W = torch.randn(cout, cin, 3, 3, generator=gen).to(DEV)
+    P = modconv.PackedConv(W, 1)
+    x = torch.randn(n, cin, r, r, device=DEV)
+    s = torch.rand(n, cin, device=DEV) + 0.5
+    ph, nph, _, _ = P.fwd_phases(r, r)
+    y = torch.empty(n, cout, r, r, device=DEV)
+    modconv.gemm(x, y, ph, nph, cin, cout, s=s, epi=modconv._epilogue(_hip.EPI_STORE))
+    y2 = torch.empty_like(y)
+    h = n // 2
+    for sl in (slice(0, h), slice(h, n)):
+        part = torch.empty(h, cout, r, r, device=DEV)
+        modconv.gemm(x[sl].contiguous(), part, ph, nph, cin, cout, s=s[sl].contiguous(),
+                     epi=modconv._epilogue(_hip.EPI_STORE))
+        y2[sl] = part
+    err = ((y - y2).abs().max() / y2.abs().max()).item()
+    assert err <= 2e-6, err
+    del x, y, y2
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("cin,res,n,clamp", [(512, 4, 2, 256.0), (64, 64, 3, 0.3), (32, 128, 1, None), (128, 9, 2, 1.0)])
