@@ -198,12 +198,13 @@ def test_synthesis_layer_grad_subsets():
 
 
 @pytest.mark.parametrize("n,cin,cout,r", [(2, 32, 32, 256), (4, 64, 32, 128), (1, 32, 32, 1024), (2, 64, 64, 128),
-                                           (1, 96, 64, 256), (1, 128, 128, 128), (1, 256, 256, 128), (2, 512, 512, 16)])
+                                           (1, 96, 64, 256), (2, 64, 64, 256), (1, 128, 128, 128), (1, 256, 256, 128),
+                                           (2, 512, 512, 16)])
 def test_conv_gemm_same3x3_vs_conv2d(n, cin, cout, r):
     """3x3 'same' convs (conv1 forward with per-sample style-scaled weights, and its data gradient with the
     shared flipped weights) against an fp64 CPU convolution (no activation, so no kinks: tolerance 2e-5 of the
-    max).  W >= 128 runs the row-halo kernel (conv_row_kernel) for every tile width (32 / 64 / 128 output
-    channels); W = 16 the tap-major LDS-DMA kernel."""
+    max).  32 / 64 output channels with W % 256 == 0 run the row-halo kernel (conv_row_kernel, both tile
+    widths); the other shapes the tap-major LDS-DMA kernel."""
     import torch.nn.functional as F
     from stylemc_amd import _hip, modconv
     gen = torch.Generator().manual_seed(11)

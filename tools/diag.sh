@@ -8,5 +8,5 @@ cat $OUT/phase.txt | tail -6
 timeout -k 10 300 python tools/aten_ops.py > $OUT/aten.txt 2>&1; stop $?
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timer > $OUT/prof.log 2>&1; stop $?
-python tools/prof_summary.py $OUT/prof/run_kernel_stats.csv --steps 7 > $OUT/summary.md
+python tools/prof_summary.py $OUT/prof/run_kernel_trace.csv --steps 7 > $OUT/summary.md
 head -40 $OUT/summary.md

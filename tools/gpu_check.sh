@@ -18,5 +18,5 @@ timeout -k 10 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline "$@" >
 grep '^{' $OUT/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('VALUE', d['value'], d['unit'], 'ms/step', d['ms_per_step'], 'roofline', d['roofline'])"
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timer > $OUT/prof.log 2>&1 || { echo "PROF FAILED"; tail -5 $OUT/prof.log; exit 1; }
-python tools/prof_summary.py $OUT/prof/run_kernel_stats.csv --steps 7 > $OUT/summary.md
+python tools/prof_summary.py $OUT/prof/run_kernel_trace.csv --steps 7 > $OUT/summary.md
 head -30 $OUT/summary.md

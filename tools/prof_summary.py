@@ -1,45 +1,61 @@
-"""Summarise a rocprofv3 --kernel-trace --stats run (kernel_stats.csv) as markdown.
+"""Summarise a rocprofv3 --kernel-trace run as markdown, per find_direction step.
 
-    python tools/prof_summary.py gpurun_out/prof1/run_kernel_stats.csv [--steps N] > profiles/rXX_summary.md
+    python tools/prof_summary.py gpurun_out/prof1/run_kernel_trace.csv --steps N > profiles/rXX_summary.md
 
+Only kernels from the first synthesis GEMM launch on are counted (model construction before it -- weight
+uploads, packing -- is not part of a step); N = the steps run from there (bench warm-up + timed steps).
 Reports the top kernels and the aggregate of the synthesis modconv GEMM family (conv_gemm_lds_kernel /
-conv_gemm_kernel / convt_gemm_kernel instantiations with TAG 0 -- the IR-SE50 executor's launches of the
-same kernels carry TAG 1 and are reported separately), whose average launch duration bench.py's
-HIP-event roofline pass must match.
+conv_gemm_kernel / conv_row_kernel / convt_gemm_kernel instantiations with TAG 0 -- the IR-SE50 executor's
+launches of the same kernels carry TAG 1 and are reported separately), whose average launch duration
+bench.py's HIP-event roofline pass must match.
 """
 import csv
 import sys
+from collections import defaultdict
+
+FAMILY = ("conv_gemm_lds_kernel", "conv_gemm_kernel", "conv_row_kernel", "convt_gemm_kernel")
+
+
+def is_family(name):
+    return any(f in name for f in FAMILY)
 
 
 def main():
     path = sys.argv[1]
-    steps = None
-    if "--steps" in sys.argv:
-        steps = int(sys.argv[sys.argv.index("--steps") + 1])
+    steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else None
     rows = list(csv.DictReader(open(path)))
-    tot = sum(float(r["TotalDurationNs"]) for r in rows)
-    print(f"# rocprofv3 kernel stats: `{path}`\n")
-    print(f"total GPU kernel time: {tot / 1e6:.2f} ms" + (f" over {steps} steps ({tot / 1e6 / steps:.2f} ms/step)" if steps else ""))
-    gemm = [r for r in rows if "conv_gemm" in r["Name"] or "convt_gemm_kernel" in r["Name"]]
-    aux = [r for r in gemm if ", 1>(" in r["Name"]]
-    fam = [r for r in gemm if r not in aux]
-    at = sum(float(r["TotalDurationNs"]) for r in aux)
-    ac = sum(int(r["Calls"]) for r in aux)
-    ft = sum(float(r["TotalDurationNs"]) for r in fam)
-    fc = sum(int(r["Calls"]) for r in fam)
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    first = next(i for i, r in enumerate(rows) if is_family(r["Kernel_Name"]))
+    rows = rows[first:]
+    tot, cnt = defaultdict(float), defaultdict(int)
+    for r in rows:
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        tot[r["Kernel_Name"]] += d
+        cnt[r["Kernel_Name"]] += 1
+    total = sum(tot.values())
+    span = int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])
+    per = f" = {total / 1e6 / steps:.2f} ms/step" if steps else ""
+    print(f"# rocprofv3 kernel trace: `{path}`\n")
+    print(f"from the first synthesis GEMM on: {len(rows)} launches, GPU kernel time {total / 1e6:.2f} ms{per} "
+          f"(summed over streams), wall span {span / 1e6:.2f} ms" + (f" = {span / 1e6 / steps:.2f} ms/step" if steps else ""))
+    fam = {k: v for k, v in tot.items() if is_family(k) and ", 1>(" not in k}
+    aux = {k: v for k, v in tot.items() if is_family(k) and ", 1>(" in k}
+    fc, ac = sum(cnt[k] for k in fam), sum(cnt[k] for k in aux)
+    ft, at = sum(fam.values()), sum(aux.values())
     if fc:
-        print(f"\nsynthesis modconv GEMM family (TAG 0: conv_gemm_lds_kernel / conv_gemm_kernel / convt_gemm_kernel): "
-              f"{fc} launches, {ft / 1e6:.2f} ms, average {ft / fc / 1e3:.1f} us/launch, {100 * ft / tot:.1f}% of GPU time")
+        print(f"\nsynthesis modconv GEMM family (TAG 0: {' / '.join(FAMILY)}): {fc} launches, {ft / 1e6:.2f} ms"
+              + (f" ({ft / 1e6 / steps:.2f} ms/step)" if steps else "")
+              + f", average {ft / fc / 1e3:.1f} us/launch, {100 * ft / total:.1f}% of GPU kernel time")
     if ac:
         print(f"IR-SE50 executor GEMMs (TAG 1): {ac} launches, {at / 1e6:.2f} ms, average {at / ac / 1e3:.1f} us/launch")
     print()
-    print("| ms total | % | calls | avg us | kernel |\n|---:|---:|---:|---:|---|")
-    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:30]:
-        name = r["Name"].replace("|", "/")
+    print("| ms total | ms/step | % | calls | avg us | kernel |\n|---:|---:|---:|---:|---:|---|")
+    for k in sorted(tot, key=lambda k: -tot[k])[:32]:
+        name = k.replace("|", "/")
         if len(name) > 110:
             name = name[:107] + "..."
-        print(f"| {float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.2f} | {r['Calls']} | "
-              f"{float(r['AverageNs']) / 1e3:.1f} | `{name}` |")
+        ps = f"{tot[k] / 1e6 / steps:.3f}" if steps else ""
+        print(f"| {tot[k] / 1e6:.2f} | {ps} | {100 * tot[k] / total:.2f} | {cnt[k]} | {tot[k] / cnt[k] / 1e3:.1f} | `{name}` |")
 
 
 if __name__ == "__main__":
