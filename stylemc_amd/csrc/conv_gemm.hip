@@ -19,6 +19,7 @@
 // workgroups into a workspace that the epilogue kernel reduces.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -867,15 +868,214 @@ __global__ __launch_bounds__(NT, 1) void convt_gemm_kernel(GemmParams p, ConvTPa
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Phase-fused stride-2 transposed 3x3 conv on LDS-DMA operands (the default for the up = 2 layers' conv).
+// Same decomposition as convt_gemm_kernel -- a workgroup owns BM super-pixels (a, b) of the (H+1) x (W+1)
+// grid and all 4 output phases, K steps are (channel chunk, input shift), and each staged shift tile feeds
+// every phase that reads it (shift 0: 4 phases, shifts 1 / 2: 2, shift 3: 1 -> the 9 taps) -- but both
+// operands go global -> LDS by DMA into a 2-stage ring as in conv_gemm_lds_kernel (no register staging, one
+// barrier per step): the input slab by `buffer_load_dword ... lds` (lane = super-pixel, the buffer range check
+// zero-fills the out-of-image shifts), the phases' weight slabs by `global_load_lds_dwordx4`.  Style scaling
+// comes in the per-sample weights (wscale_kernel) or a prescaled input, as for the other LDS-DMA launches.
+struct ConvTTaps {
+    int tap[4][4];  // [shift][phase] -> tap index in phase `phase`'s packed weights (-1: phase unused)
+};
+
+template <int S>
+__host__ __device__ constexpr int shift_phase(int j) {
+    // j-th phase reading shift S (the ShiftPhases table as a constexpr function)
+    return S == 0 ? j : (S == 1 ? (j ? 1 : 0) : (S == 2 ? (j ? 2 : 0) : 0));
+}
+
+template <int S, int TO, int TM, int BKT, int BO, int BM>
+__device__ __forceinline__ void convt_lds_mma(const float* Ws, const float* Xs, int wo, int wm, int kh, int l32,
+                                              f32x16 (&acc)[4][TO][TM]) {
+    constexpr int NP = shift_nph(S);
+    const float* wrow = Ws + kh * BO + wo * TO * 32 + l32;
+    const float* xrow = Xs + kh * BM + wm * TM * 32 + l32;
+    // software pipeline over the BKT / 2 K-pairs: the fragments of pair q + 1 are read under pair q's MFMAs
+    float af[2][NP][TO], bf[2][TM];
+    auto frag = [&](int q, int b) {
+#pragma unroll
+        for (int j = 0; j < TM; ++j) bf[b][j] = xrow[(2 * q) * BM + j * 32];
+#pragma unroll
+        for (int ph = 0; ph < NP; ++ph)
+#pragma unroll
+            for (int i = 0; i < TO; ++i) af[b][ph][i] = wrow[(ph * BKT + 2 * q) * BO + i * 32];
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int q = 0; q < BKT / 2; ++q) {
+        if (q + 1 < BKT / 2) frag(q + 1, (q + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ph = 0; ph < NP; ++ph)
+#pragma unroll
+            for (int i = 0; i < TO; ++i)
+#pragma unroll
+                for (int j = 0; j < TM; ++j)
+                    acc[shift_phase<S>(ph)][i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                        af[q & 1][ph][i], bf[q & 1][j], acc[shift_phase<S>(ph)][i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int WO, int WM, int TO, int TM, int BKT>
+__global__ __launch_bounds__(NT, 2) void convt_lds_kernel(GemmParams p, ConvTTaps tt) {
+    static_assert(WO * WM == 4, "4 waves");
+    constexpr int BO = WO * TO * 32;
+    constexpr int BM = WM * TM * 32;
+    constexpr int NCH = BM / 64;                 // 64-position chunks per input row
+    static_assert(NCH >= 1 && NCH <= 4 && 4 % NCH == 0, "BM in {64,128,256}");
+    constexpr int RSTEP = 4 / NCH;
+    constexpr int XI = BKT * NCH / 4;            // input DMAs per wave per step
+    constexpr int WSL = BKT * BO;                // floats of one phase's weight slab
+    static_assert(WSL % 256 == 0, "weight slabs split into whole 1-KB DMAs");
+    constexpr int TILE = BKT * BM + 4 * WSL;     // X slab + up to 4 phase slabs
+    __shared__ __attribute__((aligned(16))) float smem[2 * TILE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wo = wave / WM, wm = wave % WM;
+    const int gh = p.in_h + 1, gw = p.in_w + 1, hw_g = gh * gw;
+    int tm = blockIdx.x, tn = blockIdx.y;
+    if (p.ntn) {  // XCD-aware bijective tile order (see conv_gemm_lds_kernel)
+        const int nwg = gridDim.x, orig = blockIdx.x;
+        const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+        const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+        tm = wgid / p.ntn;
+        tn = wgid - tm * p.ntn;
+    }
+    int M = p.n * hw_g;
+    int m0 = tm * BM;
+    if (p.per_sample) {  // per-sample weights: tiles restart at every image
+        const int tps = (hw_g + BM - 1) / BM;
+        const int nb = tm / tps;
+        if (nb >= p.n) return;
+        m0 = nb * hw_g + (tm - nb * tps) * BM;
+        M = (nb + 1) * hw_g;
+    }
+    if (m0 >= M) return;
+    const int o0 = tn * BO;
+    const int split = blockIdx.z;
+    const int cpk = p.cin / BKT;
+    // split-K over whole channel chunks (each chunk = the 4 shift steps, unrolled below)
+    const int c_begin = (int)((int64_t)cpk * split / p.nsplit);
+    const int c_end = (int)((int64_t)cpk * (split + 1) / p.nsplit);
+    const int ks_begin = 4 * c_begin, ks_end = 4 * c_end;
+
+    const int cw = wave % NCH, r0 = wave / NCH;
+    const int m = m0 + cw * 64 + lane;
+    const bool mvalid = m < M;
+    int nn = 0, a = 0, b = 0;
+    if (mvalid) {
+        nn = m / hw_g;
+        const int rem = m - nn * hw_g;
+        a = rem / gw;
+        b = rem - a * gw;
+    }
+    const int in_hw = p.in_h * p.in_w;
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * in_hw * 4), 0x00020000);
+    const int xvbase = nn * p.cin * in_hw * 4;
+    const int wn = m0 / hw_g;  // the workgroup's sample (per-sample weights)
+
+    auto issue = [&](int ks, int slot) {
+        const int c = ks >> 2, sh = ks & 3;
+        const int ci0 = c * BKT;
+        const int iy = a - (sh & 1), ix = b - (sh >> 1);
+        const bool ok = mvalid && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w;
+        const int voff = ok ? xvbase + (iy * p.in_w + ix) * 4 : 0x7ffffff0;
+        float* xs = smem + slot * TILE;
+#pragma unroll
+        for (int j = 0; j < XI; ++j) {
+            const int row = r0 + RSTEP * j;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                xrsrc, (__attribute__((address_space(3))) void*)(xs + row * BM + cw * 64), 4, voff,
+                (ci0 + row) * in_hw * 4, 0, 0);
+        }
+        float* ws = xs + BKT * BM;
+        const int nph = shift_nph(sh);
+        for (int j = wave; j < nph * (WSL / 256); j += 4) {
+            const int pj = j / (WSL / 256);                 // which phase slab of this shift
+            const int phase = sh == 0 ? pj : (sh == 1 ? (pj ? 1 : 0) : (sh == 2 ? (pj ? 2 : 0) : 0));
+            const int f = (j - pj * (WSL / 256)) * 256 + lane * 4;
+            const int row = f / BO, col = f - row * BO;
+            const PhaseDev& q = p.ph[phase];
+            const float* src = q.wk + (q.wstride ? (int64_t)wn * q.wstride : 0) +
+                               ((int64_t)tt.tap[sh][phase] * p.cin + ci0 + row) * p.cout + o0 + col;
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(ws + pj * WSL + f - lane * 4),
+                                             16, 0, 0);
+        }
+    };
+
+    f32x16 acc[4][TO][TM];
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+        for (int i = 0; i < TO; ++i)
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[ph][i][j][r] = 0.f;
+
+    const int kh = lane >> 5, l32 = lane & 31;
+    if (ks_begin < ks_end) issue(ks_begin, 0);
+    // slot of step ks = (ks - ks_begin) & 1 = ks & 1 (ks_begin is a multiple of 4): shifts 0 / 2 in slot 0,
+    // shifts 1 / 3 in slot 1; the shift loop is unrolled so every step's phase set is a compile-time constant
+    auto step = [&](auto S_, int ks) {
+        constexpr int S = decltype(S_)::value;
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // step ks landed for every wave; the other slot is free
+        asm volatile("" ::: "memory");
+        if (ks + 1 < ks_end) issue(ks + 1, (S + 1) & 1);
+        const float* Xs = smem + (S & 1) * TILE;
+        convt_lds_mma<S, TO, TM, BKT, BO, BM>(Xs + BKT * BM, Xs, wo, wm, kh, l32, acc);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    for (int ks = ks_begin; ks < ks_end; ks += 4) {
+        step(std::integral_constant<int, 0>{}, ks);
+        step(std::integral_constant<int, 1>{}, ks + 1);
+        step(std::integral_constant<int, 2>{}, ks + 2);
+        step(std::integral_constant<int, 3>{}, ks + 3);
+    }
+
+    // epilogue: raw T (mode STORE) or this split's partial plane
+    float* dst = p.nsplit > 1 ? p.y + (int64_t)split * p.split_stride : p.y;
+    const int64_t plane = (int64_t)p.y_h * p.y_w;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+        const int mc = m0 + wm * TM * 32 + j * 32 + l32;
+        if (mc >= M) continue;
+        const int en = mc / hw_g;
+        const int erem = mc - en * hw_g;
+        const int ea = erem / gw;
+        const int eb = erem - ea * gw;
+#pragma unroll
+        for (int i = 0; i < TO; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = o0 + wo * TO * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                float* row0 = dst + ((int64_t)en * p.cout + o) * plane + (int64_t)(2 * ea) * p.y_w + 2 * eb;
+                row0[0] = acc[0][i][j][r];
+                if (eb < p.in_w) row0[1] = acc[1][i][j][r];
+                if (ea < p.in_h) {
+                    row0[p.y_w] = acc[2][i][j][r];
+                    if (eb < p.in_w) row0[p.y_w + 1] = acc[3][i][j][r];
+                }
+            }
+        }
+    }
+}
+
 // Does this 4-phase description match the polyphase stride-2 transposed 3x3 conv built by
 // stylemc_amd.modconv.PackedConv (phase index py*2+px, taps at shifts {0,-1}^2)?  Fills the table.
-bool convt_fusable(int cin, int cout, int in_h, int in_w, int y_h, int y_w, const smc_conv_phase* ph, int nph,
-                   const smc_conv_epilogue* epi, ConvTParams* q) {
+bool convt_structure(int cin, int cout, int in_h, int in_w, int y_h, int y_w, const smc_conv_phase* ph, int nph,
+                     const smc_conv_epilogue* epi, ConvTParams* q) {
     if (nph != 4 || y_h != 2 * in_h + 1 || y_w != 2 * in_w + 1) return false;
     if (epi && (epi->mode != SMC_EPI_STORE || epi->residual)) return false;
-    // measured (tools/bench_gemm.py): the fused kernel (1 wave/SIMD, 128 accumulators) wins only on the
-    // 32-channel 1024-px layer (51 vs 42 TF/s); the per-phase kernel is faster on every wider layer.
-    if (cout > 32) return false;
     ConvTParams t{};
     int count = 0;
     for (int k = 0; k < 4; ++k) {
@@ -901,6 +1101,14 @@ bool convt_fusable(int cin, int cout, int in_h, int in_w, int y_h, int y_w, cons
     return true;
 }
 
+// The register-staged fused kernel: only where the LDS-DMA one cannot run (inputs of 2 GiB or more), and
+// only for 32 output channels (1 wave/SIMD, 128 accumulators: slower than the per-phase kernel on every
+// wider layer, tools/bench_gemm.py).
+bool convt_fusable(int cin, int cout, int in_h, int in_w, int y_h, int y_w, const smc_conv_phase* ph, int nph,
+                   const smc_conv_epilogue* epi, ConvTParams* q) {
+    return cout <= 32 && convt_structure(cin, cout, in_h, in_w, y_h, y_w, ph, nph, epi, q);
+}
+
 struct ConvTCfg {
     int bo, bm, id;
 };
@@ -922,6 +1130,39 @@ int plan_split_convt(int n, int cin, int cout, int in_h, int in_w) {
     if (blocks >= target) return 1;
     int s = (int)smc::ceil_div(target, blocks > 0 ? blocks : 1);
     int cap = ks / 4;
+    if (cap > 16) cap = 16;
+    if (s > cap) s = cap;
+    return s < 1 ? 1 : s;
+}
+
+// convt_lds_kernel: the 4-phase stride-2 transposed conv of modconv.PackedConv (epilogue STORE: the blur +
+// modconv epilogue follow in smc_modconv_blur_act_f32), 32-bit input offsets, whole column tiles.
+struct ConvTL {
+    int bo, bm, id;
+};
+
+bool convt_lds_plan(int n, int cin, int cout, int in_h, int in_w, int y_h, int y_w, const smc_conv_phase* ph, int nph,
+                    const smc_conv_epilogue* epi, ConvTTaps* tt, ConvTL* cfg) {
+    ConvTParams q{};
+    if (!convt_structure(cin, cout, in_h, in_w, y_h, y_w, ph, nph, epi, &q)) return false;
+    if (cin % 16 != 0 || cout % 32 != 0 || (int64_t)n * cin * in_h * in_w * 4 >= (1LL << 31)) return false;
+    if (tt) {
+        for (int sh = 0; sh < 4; ++sh)
+            for (int k = 0; k < 4; ++k)
+                tt->tap[sh][k] = q.w[sh][k] ? (int)((q.w[sh][k] - ph[k].wk) / ((int64_t)cin * cout)) : -1;
+    }
+    if (cfg) *cfg = cout % 64 == 0 ? ConvTL{64, 128, 1} : ConvTL{32, 128, 0};
+    return true;
+}
+
+int plan_split_convt_lds(int n, int cin, int cout, int in_h, int in_w, const ConvTL& c, bool per_sample) {
+    const int64_t hw_g = (int64_t)(in_h + 1) * (in_w + 1);
+    const int64_t mt = per_sample ? n * smc::ceil_div(hw_g, c.bm) : smc::ceil_div(n * hw_g, c.bm);
+    const int64_t blocks = mt * (cout / c.bo);
+    const int64_t target = 2LL * smc::device_cu_count();
+    if (blocks >= target) return 1;
+    int s = (int)smc::ceil_div(target, blocks > 0 ? blocks : 1);
+    int cap = (cin / 16) / 2;   // whole channel chunks per split, at least two
     if (cap > 16) cap = 16;
     if (s > cap) s = cap;
     return s < 1 ? 1 : s;
@@ -1077,8 +1318,13 @@ SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, 
     Cfg c;
     if (pick_cfg(cout, &c) < 0 || cin % BK != 0 || nphases < 1 || nphases > 4 || !phases) return 0;
     int s;
+    ConvTL tl;
     if (nphases == 4 && y_h % 2 == 1 && y_w % 2 == 1 &&
-        convt_fusable(cin, cout, (y_h - 1) / 2, (y_w - 1) / 2, y_h, y_w, phases, nphases, nullptr, nullptr))
+        convt_lds_plan(n, cin, cout, (y_h - 1) / 2, (y_w - 1) / 2, y_h, y_w, phases, nphases, nullptr, nullptr, &tl))
+        s = std::max(plan_split_convt_lds(n, cin, cout, (y_h - 1) / 2, (y_w - 1) / 2, tl, true),
+                     plan_split_convt_lds(n, cin, cout, (y_h - 1) / 2, (y_w - 1) / 2, tl, false));
+    else if (nphases == 4 && y_h % 2 == 1 && y_w % 2 == 1 &&
+             convt_fusable(cin, cout, (y_h - 1) / 2, (y_w - 1) / 2, y_h, y_w, phases, nphases, nullptr, nullptr))
         s = plan_split_convt(n, cin, cout, (y_h - 1) / 2, (y_w - 1) / 2);
     else
         s = plan_split(n, cin, cout, phases, nphases, c);
@@ -1105,17 +1351,23 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     Cfg c;
     int cfg = pick_cfg(cout, &c);
     ConvTParams ctp{};
-    const bool fused_t = convt_fusable(cin, cout, in_h, in_w, y_h, y_w, phases, nphases, epi, &ctp);
+    ConvTTaps ctt{};
+    ConvTL tl{};
+    const bool convt_lds = convt_lds_plan(n, cin, cout, in_h, in_w, y_h, y_w, phases, nphases, epi, &ctt, &tl);
+    const bool fused_t = !convt_lds && convt_fusable(cin, cout, in_h, in_w, y_h, y_w, phases, nphases, epi, &ctp);
     const int64_t pre_fl = prescale_floats(n, cin, cout, phases, nphases);
     const bool prescale = s_in && !fused_t && pre_fl > 0 && (int64_t)n * cin * in_h * in_w <= pre_fl &&
                           (in_h * in_w) % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     const float* s_prescale = s_in;
     if (prescale) s_in = nullptr;  // the GEMM reads x * s from the workspace with the shared weights
-    if (!fused_t && small_tile_ok(n, cin, cout, in_h, in_w, phases, nphases, s_in != nullptr, c)) {
+    if (!fused_t && !convt_lds && small_tile_ok(n, cin, cout, in_h, in_w, phases, nphases, s_in != nullptr, c)) {
         cfg = 3;
         c = Cfg{64, 64};
     }
-    const int nsplit = fused_t ? plan_split_convt(n, cin, cout, in_h, in_w) : plan_split(n, cin, cout, phases, nphases, c);
+    const bool t_per_sample = convt_lds && s_in && ((int64_t)(in_h + 1) * (in_w + 1)) % tl.bm != 0;
+    const int nsplit = convt_lds ? plan_split_convt_lds(n, cin, cout, in_h, in_w, tl, t_per_sample)
+                                 : fused_t ? plan_split_convt(n, cin, cout, in_h, in_w)
+                                           : plan_split(n, cin, cout, phases, nphases, c);
     const int64_t plane_elems = (int64_t)n * cout * y_h * y_w;
     if (nsplit > 1) {
         const int64_t need = nsplit * plane_elems * (int64_t)sizeof(float);
@@ -1172,6 +1424,42 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     p.split_stride = plane_elems;
 
     hipStream_t st = smc::as_stream(stream);
+    // per-sample weights W[t][i][o] * s[n][i], [phase][n][taps*cin][cout], after the split-K partials
+    auto make_wsample = [&]() -> int {
+        const int64_t part = nsplit > 1 ? ((nsplit * plane_elems * (int64_t)sizeof(float) + 255) / 256) * 256 : 0;
+        const int64_t need = part + wsample_floats(n, cin, cout, phases, nphases) * (int64_t)sizeof(float);
+        SMC_CHECK(workspace && workspace_bytes >= need, "smc_conv_gemm_f32: workspace %lld < %lld bytes",
+                  (long long)workspace_bytes, (long long)need);
+        float* wsamp = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + part);
+        int64_t off = 0;
+        for (int i = 0; i < nphases; ++i) {
+            const int rows = phases[i].ntaps * cin;
+            const int64_t tot4 = (int64_t)rows * cout / 4 * n;
+            hipLaunchKernelGGL(wscale_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(tot4, 256), 4096)),
+                               dim3(256), 0, st, phases[i].wk, s_in, wsamp + off, rows, cin, cout, n);
+            p.ph[i].wk = wsamp + off;
+            p.ph[i].wstride = (int64_t)rows * cout;
+            off += (int64_t)rows * cout * n;
+        }
+        return smc::check_launch("smc_conv_gemm_f32 (per-sample weights)");
+    };
+    if (convt_lds) {
+        if (s_in) {
+            rc = make_wsample();
+            if (rc != SMC_OK) return rc;
+        }
+        p.s = nullptr;
+        const int64_t hw_g = (int64_t)(in_h + 1) * (in_w + 1);
+        const int64_t mt = t_per_sample ? n * smc::ceil_div(hw_g, tl.bm) : smc::ceil_div(n * hw_g, tl.bm);
+        p.per_sample = t_per_sample ? 1 : 0;
+        p.ntn = cout / tl.bo;
+        dim3 g((unsigned)(mt * p.ntn), 1, (unsigned)nsplit);
+        if (tl.id == 1) hipLaunchKernelGGL((convt_lds_kernel<2, 2, 1, 2, 16>), g, dim3(NT), 0, st, p, ctt);
+        else hipLaunchKernelGGL((convt_lds_kernel<1, 4, 1, 1, 16>), g, dim3(NT), 0, st, p, ctt);
+        rc = smc::check_launch("smc_conv_gemm_f32 (fused transposed conv, LDS-DMA)");
+        if (rc != SMC_OK || nsplit == 1) return rc;
+        return smc_modconv_epilogue_f32(workspace, nsplit, plane_elems, y, n, cout, y_h, y_w, &e, stream);
+    }
     if (fused_t) {
         const ConvTCfg tc = convt_cfg(cout);
         const int64_t M = (int64_t)n * (in_h + 1) * (in_w + 1);
@@ -1202,23 +1490,7 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             p.per_sample = 1;
         }
         if (s_in) {
-            // per-sample weights W[t][i][o] * s[n][i], [phase][n][taps*cin][cout], after the split-K partials
-            const int64_t part = nsplit > 1 ? ((nsplit * plane_elems * (int64_t)sizeof(float) + 255) / 256) * 256 : 0;
-            const int64_t need = part + wsample_floats(n, cin, cout, phases, nphases) * (int64_t)sizeof(float);
-            SMC_CHECK(workspace && workspace_bytes >= need, "smc_conv_gemm_f32: workspace %lld < %lld bytes",
-                      (long long)workspace_bytes, (long long)need);
-            float* wsamp = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + part);
-            int64_t off = 0;
-            for (int i = 0; i < nphases; ++i) {
-                const int rows = phases[i].ntaps * cin;
-                const int64_t tot4 = (int64_t)rows * cout / 4 * n;
-                hipLaunchKernelGGL(wscale_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(tot4, 256), 4096)),
-                                   dim3(256), 0, st, phases[i].wk, s_in, wsamp + off, rows, cin, cout, n);
-                p.ph[i].wk = wsamp + off;
-                p.ph[i].wstride = (int64_t)rows * cout;
-                off += (int64_t)rows * cout * n;
-            }
-            rc = smc::check_launch("smc_conv_gemm_f32 (per-sample weights)");
+            rc = make_wsample();
             if (rc != SMC_OK) return rc;
         }
         p.s = nullptr;

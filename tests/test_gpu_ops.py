@@ -225,6 +225,27 @@ def test_conv_gemm_same3x3_vs_conv2d(n, cin, cout, r):
     close(dx, refb, 2e-5, "data grad")
 
 
+@pytest.mark.parametrize("n,cin,cout,h", [(2, 64, 32, 64), (1, 128, 64, 128), (2, 512, 512, 4), (3, 256, 128, 16),
+                                           (1, 512, 256, 32), (2, 32, 32, 33), (4, 512, 512, 8)])
+def test_conv_gemm_transposed_vs_conv_transpose2d(n, cin, cout, h):
+    """The up = 2 layers' stride-2 transposed 3x3 conv (conv2d_resample.py:125-138 before the blur) as the
+    phase-fused LDS-DMA kernel: per-sample style-scaled weights with tiles restarted per image ((h+1)^2 not a
+    tile multiple), a prescaled input at the low resolutions, split-K over channel chunks; vs fp64
+    conv_transpose2d (tolerance 2e-5 of the max)."""
+    import torch.nn.functional as F
+    from stylemc_amd import _hip, modconv
+    gen = torch.Generator().manual_seed(13)
+    W = torch.randn(cout, cin, 3, 3, generator=gen)
+    P = modconv.PackedConv(W.to(DEV), 2)
+    x = torch.randn(n, cin, h, h, generator=gen)
+    s = torch.randn(n, cin, generator=gen) * 0.5 + 1
+    ph, nph, th, tw = P.fwd_phases(h, h)
+    t = torch.empty(n, cout, th, tw, device=DEV)
+    modconv.gemm(x.to(DEV), t, ph, nph, cin, cout, s=s.to(DEV), epi=modconv._epilogue(_hip.EPI_STORE))
+    ref = F.conv_transpose2d((x * s[:, :, None, None]).double(), W.transpose(0, 1).double(), stride=2)
+    close(t, ref, 2e-5, "transposed conv")
+
+
 def test_conv_gemm_2gib_input_fallback():
     """An input of >= 2 GiB (batch 16 of the r = 1024 conv1: 2.1 GB) exceeds the 32-bit buffer offsets of the
     LDS-DMA / row-halo kernels and runs the register-staged kernel with 64-bit addressing: it must equal the
