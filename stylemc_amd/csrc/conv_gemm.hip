@@ -1501,12 +1501,12 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         RowTaps rt{};
         if (nsplit == 1 && !p.per_sample && (cfg == 4 || cfg == 5) &&
             row_ok(n, cin, cout, in_h, in_w, y_h, y_w, phases, nphases, Cfg{c.bo, 256}, &rt)) {
-            p.ntn = 1;
+            p.ntn = cout / c.bo;  // column tiles (a 96-channel data gradient: 3 x 32)
             // measured on MI355X (tools/bench_gemm.py, batch 4; tap-major kernel in brackets): 32 channels,
             // 32 x 256 tiles of 8-channel steps: r = 1024 conv1 710 / 701 us fwd / data grad (840 / 818); 64
             // channels, 64 x 256: r = 512 655 / 648 (688 / 679).  128+ channels stay tap-major (the 128 x 128
             // row tile: 690 vs 634 us at r = 256).
-            const int tiles = (int)(((int64_t)n * in_h * in_w) / 256);
+            const int tiles = (int)(((int64_t)n * in_h * in_w) / 256) * p.ntn;
             if (cfg == 4) hipLaunchKernelGGL((conv_row_kernel<1, 4, 1, 2, 8>), dim3(tiles), dim3(NT), 0, st, p, rt);
             else hipLaunchKernelGGL((conv_row_kernel<1, 4, 2, 2, 8>), dim3(tiles), dim3(NT), 0, st, p, rt);
             return smc::check_launch("smc_conv_gemm_f32 (row-halo)");

@@ -158,6 +158,41 @@ def _pair_layers(cin, cout, res, up, clamp, seed=0, kind="conv"):
     return o.eval(), p.to(DEV).eval()
 
 
+def kink_footprint(y_ref, up, clamp=None, rel=1e-5):
+    """Input positions [n, h, w] whose gradient may legitimately differ between two fp32 evaluations: an
+    output element within `rel` (of the output scale) of an activation kink (lrelu at 0, the clamp) can take
+    either branch, and that one flipped derivative reaches every input channel at every position of the conv
+    adjoint's footprint (3x3, or for up = 2 the 4x4 blur adjoint then the stride-2 3x3 gather: dilate 2)."""
+    y = y_ref.detach().double().cpu()
+    sc = y.abs().max().item()
+    amb = (y.abs() <= rel * sc)
+    if clamp is not None:
+        amb |= ((y.abs() - clamp).abs() <= rel * sc)
+    amb = amb.any(dim=1).double()[:, None]
+    if up == 2:
+        amb = F_pool(amb, 2)
+    k = 5 if up == 2 else 3
+    return torch.nn.functional.max_pool2d(amb, k, stride=1, padding=k // 2)[:, 0] > 0
+
+
+def F_pool(t, k):
+    return torch.nn.functional.max_pool2d(t, k, stride=k)
+
+
+def close_grad_outside(a, b, foot, tol, what=""):
+    """close_grad for an input gradient, excluding the kink footprint (kink_footprint); that footprint must
+    stay a small part of the tensor (<= 5 % of the positions)."""
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    assert foot.double().mean().item() <= 0.05, f"{what}: kink footprint {foot.double().mean().item():.3f}"
+    keep = ~foot[:, None].expand_as(b)
+    scale = max(b.abs().max().item(), 1e-12)
+    err = (a - b).abs()[keep]
+    assert err.numel() == 0 or err.max().item() <= tol * scale, f"{what}: max err {err.max():.3e} > {tol:.1e} * {scale:.3e}"
+    rel = ((a - b)[keep].norm() / max(b[keep].norm().item(), 1e-30)).item()
+    assert rel <= tol, f"{what}: relative norm error {rel:.3e} > {tol:.1e}"
+
+
 @pytest.mark.parametrize("cin,cout,res,up,n", [
     (32, 32, 16, 1, 2), (64, 32, 32, 2, 2), (512, 512, 4, 1, 3), (512, 512, 8, 2, 2), (128, 64, 64, 1, 1),
     (256, 128, 32, 2, 1), (512, 256, 16, 2, 4),
@@ -176,8 +211,9 @@ def test_synthesis_layer_vs_oracle(cin, cout, res, up, n, noise_mode):
     yg = p(xg, sg, noise_mode=noise_mode)
     dxg, dsg = torch.autograd.grad((yg * cot.to(DEV)).sum(), [xg, sg])
     close(yg, yr, 2e-5, "y")
-    close_grad(dxg, dxr, 1e-4, "dx")
-    close_grad(dsg, dsr, 1e-4, "ds", max_flips=0)
+    foot = kink_footprint(yr, up, o.conv_clamp)
+    close_grad_outside(dxg, dxr, foot, 1e-4, "dx")
+    close_grad(dsg, dsr, 1e-4 if not foot.any() else 2e-3, "ds", max_flips=0)
 
 
 def test_synthesis_layer_grad_subsets():
