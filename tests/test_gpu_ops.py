@@ -158,16 +158,17 @@ def _pair_layers(cin, cout, res, up, clamp, seed=0, kind="conv"):
     return o.eval(), p.to(DEV).eval()
 
 
-def kink_footprint(y_ref, up, clamp=None, rel=1e-5):
-    """Input positions [n, h, w] whose gradient may legitimately differ between two fp32 evaluations: an
-    output element within `rel` (of the output scale) of an activation kink (lrelu at 0, the clamp) can take
-    either branch, and that one flipped derivative reaches every input channel at every position of the conv
-    adjoint's footprint (3x3, or for up = 2 the 4x4 blur adjoint then the stride-2 3x3 gather: dilate 2)."""
-    y = y_ref.detach().double().cpu()
-    sc = y.abs().max().item()
-    amb = (y.abs() <= rel * sc)
+def kink_footprint(y_gpu, y_ref, up, clamp=None):
+    """Input positions [n, h, w] whose gradient may legitimately differ between the two fp32 evaluations: an
+    output element whose pre-activation sits within rounding of an activation kink (lrelu at 0, the clamp)
+    can take the other branch on one side -- visible as a different sign, or a different clamped state, of
+    the two outputs -- and that one flipped derivative reaches every input channel at every position of the
+    conv adjoint's footprint (3x3, or for up = 2 the 4x4 blur adjoint then the stride-2 3x3 gather: dilate 2)."""
+    a = y_gpu.detach().double().cpu()
+    b = y_ref.detach().double().cpu()
+    amb = (a > 0) != (b > 0)
     if clamp is not None:
-        amb |= ((y.abs() - clamp).abs() <= rel * sc)
+        amb |= (a.abs() >= clamp) != (b.abs() >= clamp)
     amb = amb.any(dim=1).double()[:, None]
     if up == 2:
         amb = F_pool(amb, 2)
@@ -211,7 +212,7 @@ def test_synthesis_layer_vs_oracle(cin, cout, res, up, n, noise_mode):
     yg = p(xg, sg, noise_mode=noise_mode)
     dxg, dsg = torch.autograd.grad((yg * cot.to(DEV)).sum(), [xg, sg])
     close(yg, yr, 2e-5, "y")
-    foot = kink_footprint(yr, up, o.conv_clamp)
+    foot = kink_footprint(yg, yr, up, o.conv_clamp)
     close_grad_outside(dxg, dxr, foot, 1e-4, "dx")
     close_grad(dsg, dsr, 1e-4 if not foot.any() else 2e-3, "ds", max_flips=0)
 
