@@ -169,6 +169,8 @@ def kink_footprint(y_gpu, y_ref, up, clamp=None):
     amb = (a > 0) != (b > 0)
     if clamp is not None:
         amb |= (a.abs() >= clamp) != (b.abs() >= clamp)
+    namb = int(amb.sum())
+    assert namb <= max(2, amb.numel() // 1000), f"{namb} outputs on different sides of a kink"
     amb = amb.any(dim=1).double()[:, None]
     if up == 2:
         amb = F_pool(amb, 2)
@@ -181,11 +183,10 @@ def F_pool(t, k):
 
 
 def close_grad_outside(a, b, foot, tol, what=""):
-    """close_grad for an input gradient, excluding the kink footprint (kink_footprint); that footprint must
-    stay a small part of the tensor (<= 5 % of the positions)."""
+    """close_grad for an input gradient, excluding the kink footprint (kink_footprint, which bounds the number
+    of disagreeing outputs)."""
     a = a.detach().double().cpu()
     b = b.detach().double().cpu()
-    assert foot.double().mean().item() <= 0.05, f"{what}: kink footprint {foot.double().mean().item():.3f}"
     keep = ~foot[:, None].expand_as(b)
     scale = max(b.abs().max().item(), 1e-12)
     err = (a - b).abs()[keep]
