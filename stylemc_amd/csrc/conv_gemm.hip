@@ -1145,7 +1145,10 @@ bool convt_lds_plan(int n, int cin, int cout, int in_h, int in_w, int y_h, int y
                     const smc_conv_epilogue* epi, ConvTTaps* tt, ConvTL* cfg) {
     ConvTParams q{};
     if (!convt_structure(cin, cout, in_h, in_w, y_h, y_w, ph, nph, epi, &q)) return false;
-    if (cin % 16 != 0 || cout % 32 != 0 || (int64_t)n * cin * in_h * in_w * 4 >= (1LL << 31)) return false;
+    // measured (tools/bench_gemm.py, batch 4): r = 1024 (64 -> 32 ch) 615 -> 413 us, r = 512 (128 -> 64) 427 ->
+    // 416 us against the per-phase kernel; from 128 output channels up the per-phase kernel stays ahead
+    // (r = 256: 364 vs 434 us; the 4 phases' accumulators cost the wide tiles their occupancy)
+    if (cin % 16 != 0 || cout % 32 != 0 || cout > 64 || (int64_t)n * cin * in_h * in_w * 4 >= (1LL << 31)) return false;
     if (tt) {
         for (int sh = 0; sh < 4; ++sh)
             for (int k = 0; k < 4; ++k)
