@@ -130,20 +130,22 @@ int smc_modconv_epilogue_f32(const float* src, int nsplit, int64_t split_stride,
                              int w, const smc_conv_epilogue* epi, void* stream);
 
 /* Fused conv0 epilogue: U = upfirdn2d(T, f, pad=(padx0,pady0 on both sides), gain=fgain) (1:1 FIR),
- * then the modconv epilogue (u_save receives U).  T: [n, c, t_h, t_w] (may be `nsplit` partial
- * planes), y: [n, c, y_h, y_w].  Only the 4x4 FIR of the [1,3,3,1] resample filter has a fused kernel;
- * other sizes return SMC_ERR_UNSUPPORTED. */
+ * then the modconv epilogue (u_save receives U).  T: [n, c, t_h, t_pitch] of which the first t_w columns
+ * are the image (t_pitch = 0: t_w; a pitch that is a multiple of 4 -- the transposed conv's odd 2h + 1
+ * width padded -- takes the 16-B load path), may be `nsplit` partial planes; y: [n, c, y_h, y_w].  Only
+ * the 4x4 FIR of the [1,3,3,1] resample filter has a fused kernel; other sizes return SMC_ERR_UNSUPPORTED. */
 int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_stride, float* y, int n, int c, int t_h,
-                             int t_w, int y_h, int y_w, const float* f, int fh, int fw, int padx0, int pady0,
-                             float fgain, int flip, const smc_conv_epilogue* epi, void* stream);
+                             int t_w, int t_pitch, int y_h, int y_w, const float* f, int fh, int fw, int padx0,
+                             int pady0, float fgain, int flip, const smc_conv_epilogue* epi, void* stream);
 
 /* Backward of smc_modconv_blur_act_f32 in one pass: du = bias_act'(g; y re-derived from u) * d[n,o],
  * dt = adjoint FIR of du (pad (pady0, padx0) = (fh-1-p, fw-1-p) of the forward pad p, flip, gain fgain;
  * upfirdn2d.py:245-264 rule), and if dd != NULL: dd[n,o] += sum_hw dz*u.  g/u: [n,c,u_h,u_w],
- * dt: [n,c,t_h,t_w].  4x4 filters only (SMC_ERR_UNSUPPORTED otherwise). */
+ * dt: [n,c,t_h,t_pitch] (t_pitch = 0: t_w; columns >= t_w are not written).  4x4 filters only
+ * (SMC_ERR_UNSUPPORTED otherwise). */
 int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* dt, float* dd, int n, int c, int u_h, int u_w,
-                                 int t_h, int t_w, const float* f, int fh, int fw, int padx0, int pady0, float fgain,
-                                 int flip, const smc_conv_epilogue* epi, void* stream);
+                                 int t_h, int t_w, int t_pitch, const float* f, int fh, int fw, int padx0, int pady0,
+                                 float fgain, int flip, const smc_conv_epilogue* epi, void* stream);
 
 /* d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps), wsq[o,i] = sum_k W[o,i,k]^2 (demodulation). */
 int smc_modconv_demod_f32(const float* s, const float* wsq, float* d, int n, int cin, int cout, float eps,

@@ -56,10 +56,10 @@ _SIGS = {
     "smc_conv_gemm_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, c_int64,
                                   P]),
     "smc_modconv_epilogue_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, P, P]),
-    "smc_modconv_blur_act_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int,
-                                         c_int, c_int, c_int, c_float, c_int, P, P]),
-    "smc_modconv_blur_act_bwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int,
-                                             c_int, c_int, c_float, c_int, P, P]),
+    "smc_modconv_blur_act_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
+                                         c_int, c_int, c_int, c_int, c_float, c_int, P, P]),
+    "smc_modconv_blur_act_bwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int,
+                                             c_int, c_int, c_int, c_float, c_int, P, P]),
     "smc_modconv_demod_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "smc_modconv_act_bwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P]),
     "smc_channel_dot_f32": (c_int, [P, P, P, P, P, c_int64, c_int64, c_int, P]),

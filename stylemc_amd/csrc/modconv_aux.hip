@@ -93,9 +93,9 @@ constexpr int kBT = 32;        // output tile (kBT x kBT), 256 threads x 4 rows
 constexpr int kMaxF = 8;
 
 __global__ __launch_bounds__(256) void blur_act_kernel(const float* t, int nsplit, int64_t split_stride, float* y,
-                                                       int c, int t_h, int t_w, int y_h, int y_w, const float* f,
-                                                       int fh, int fw, int padx0, int pady0, float fgain, int flip,
-                                                       Epi e) {
+                                                       int c, int t_h, int t_w, int tp_w, int y_h, int y_w,
+                                                       const float* f, int fh, int fw, int padx0, int pady0, float fgain,
+                                                       int flip, Epi e) {
     __shared__ float tile[(kBT + kMaxF - 1) * (kBT + kMaxF - 1)];
     __shared__ float taps[kMaxF * kMaxF];
     const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
@@ -108,13 +108,13 @@ __global__ __launch_bounds__(256) void blur_act_kernel(const float* t, int nspli
     }
     const int rows = kBT + fh - 1, cols = kBT + fw - 1;
     const int iy0 = oy0 - pady0, ix0 = ox0 - padx0;
-    const float* tp = t + nc * (int64_t)t_h * t_w;
+    const float* tp = t + nc * (int64_t)t_h * tp_w;
     for (int i = tid; i < rows * cols; i += 256) {
         const int r = i / cols, cc = i - r * cols;
         const int iy = iy0 + r, ix = ix0 + cc;
         float v = 0.f;
         if (iy >= 0 && iy < t_h && ix >= 0 && ix < t_w) {
-            const int64_t off = (int64_t)iy * t_w + ix;
+            const int64_t off = (int64_t)iy * tp_w + ix;
             v = tp[off];
             for (int s = 1; s < nsplit; ++s) v += tp[s * split_stride + off];
         }
@@ -215,8 +215,8 @@ __device__ __forceinline__ void load_taps(const float* f, int flip, float fgain,
 // Forward conv0 epilogue: U = FIR(T) (1:1, pad (pady0, padx0)), y = epi(U); stores y and U.
 template <int FH, int FW>
 __global__ __launch_bounds__(256) void blur_act_fast(const float* t, int nsplit, int64_t split_stride, float* y, int c,
-                                                     int t_h, int t_w, int y_h, int y_w, const float* f, int padx0,
-                                                     int pady0, float fgain, int flip, Epi e) {
+                                                     int t_h, int t_w, int tp_w, int y_h, int y_w, const float* f,
+                                                     int padx0, int pady0, float fgain, int flip, Epi e) {
     constexpr int ROWS = kFH + FH - 1, COLS = kFW + FW - 1, STRIDE = COLS + 1;
     __shared__ float tile[ROWS * STRIDE];
     const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256) void blur_act_fast(const float* t, int nsplit,
     float tp[FH][FW];
     load_taps<FH, FW>(f, flip, fgain, tp);
     const int iy0 = oy0 - pady0, ix0 = ox0 - padx0;
-    const float* tpl = t + nc * (int64_t)t_h * t_w;
+    const float* tpl = t + nc * (int64_t)t_h * tp_w;
     // Haloed tile load with a fixed, unrolled trip count: every load of the thread is in flight before
     // the first LDS store (a data-dependent loop serialises one HBM latency per element).  Out-of-range
     // elements load the plane's first float (always valid) and are zeroed by select.
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void blur_act_fast(const float* t, int nsplit,
         const int r = i / COLS, cc = i - r * COLS;
         const int iy = iy0 + r, ix = ix0 + cc;
         const bool ok = i < ROWS * COLS && iy >= 0 && iy < t_h && ix >= 0 && ix < t_w;
-        off[l] = ok ? iy * t_w + ix : -1;
+        off[l] = ok ? iy * tp_w + ix : -1;
         const float a = tpl[ok ? off[l] : 0];
         v[l] = ok ? a : 0.f;
     }
@@ -307,12 +307,102 @@ __global__ __launch_bounds__(256) void blur_act_fast(const float* t, int nsplit,
     }
 }
 
+// blur_act_fast with 16-B loads.  Each haloed tile row is fetched as the 16-B aligned float4 groups (aligned in the
+// buffer, so any row pitch works -- the transposed conv's odd 2h + 1 width included) that cover
+// [ox0 - 4, ox0 + kFW + 4): a third of the load instructions of the scalar form, every one a full 16 B; the groups'
+// elements outside the tile window, the image width or the row are dropped / zeroed on the way into LDS.
+// Needs a 16-B aligned t, split_stride % 4 == 0, padx0 <= 4 and FW - 1 - padx0 <= 4.
+template <int FH, int FW>
+__global__ __launch_bounds__(256) void blur_act_v4(const float* t, int nsplit, int64_t split_stride, float* y, int c,
+                                                   int t_h, int t_w, int tp_w, int y_h, int y_w, const float* f,
+                                                   int padx0, int pady0, float fgain, int flip, Epi e) {
+    constexpr int ROWS = kFH + FH - 1, COLS = kFW + FW - 1, STRIDE = COLS + 1;
+    constexpr int G4 = (kFW + 8) / 4 + 1;               // float4 groups per tile row (+1: row misalignment)
+    constexpr int NL = (ROWS * G4 + 255) / 256;
+    __shared__ float tile[ROWS * STRIDE];
+    const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
+    const int ox0 = blockIdx.x * kFW, oy0 = blockIdx.y * kFH;
+    const int64_t nc = blockIdx.z;
+    const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
+    float tp[FH][FW];
+    load_taps<FH, FW>(f, flip, fgain, tp);
+    const int iy0 = oy0 - pady0, ix0 = ox0 - padx0;
+    const int64_t pbase = nc * (int64_t)t_h * tp_w;
+    float4 v[NL];
+    int64_t off[NL];   // buffer index of the group's first element, -1: no valid element
+    int gx[NL];        // image column of the group's first element
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        const int i = tid + 256 * l;
+        const int r = i / G4, q = i - r * G4;
+        const int iy = iy0 + r;
+        const int64_t row = pbase + (int64_t)iy * tp_w;
+        const int64_t g0 = ((row + ox0 - 4) & ~(int64_t)3) + 4 * q;
+        gx[l] = (int)(g0 - row);
+        const bool ok = i < ROWS * G4 && iy >= 0 && iy < t_h && gx[l] + 3 >= 0 && gx[l] < t_w;
+        off[l] = ok ? g0 : -1;
+        v[l] = *reinterpret_cast<const float4*>(t + (ok ? g0 : 0));
+    }
+    for (int s = 1; s < nsplit; ++s) {
+        const float* sp = t + s * split_stride;
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            const float4 a = *reinterpret_cast<const float4*>(sp + (off[l] >= 0 ? off[l] : 0));
+            v[l].x += a.x; v[l].y += a.y; v[l].z += a.z; v[l].w += a.w;
+        }
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        const int i = tid + 256 * l;
+        if (i >= ROWS * G4) continue;
+        const int r = i / G4;
+        const float a[4] = {v[l].x, v[l].y, v[l].z, v[l].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int ix = gx[l] + k;
+            const int cc = ix - ix0;
+            if (cc >= 0 && cc < COLS) tile[r * STRIDE + cc] = (off[l] >= 0 && ix >= 0 && ix < t_w) ? a[k] : 0.f;
+        }
+    }
+    __syncthreads();
+    float out[4][2];
+    fir_block<FH, FW>(tile, STRIDE, 4 * ty, 2 * tx, tp, out);
+    const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
+    const float dv = e.d ? e.d[nc] : 1.f;
+    const float bv = e.bias ? e.bias[o] : 0.f;
+    const int64_t plane = nc * (int64_t)y_h * y_w;
+    const int ox = ox0 + 2 * tx;
+    if (ox >= y_w) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int oy = oy0 + 4 * ty + i;
+        if (oy >= y_h) continue;
+        const int64_t pix = (int64_t)oy * y_w + ox;
+        const float2 u2 = make_float2(out[i][0], out[i][1]);
+        if (e.mode == SMC_EPI_STORE) {
+            *reinterpret_cast<float2*>(y + plane + pix) = u2;
+            continue;
+        }
+        if (e.u_save) *reinterpret_cast<float2*>(e.u_save + plane + pix) = u2;
+        float2 nz = make_float2(0.f, 0.f);
+        if (e.noise) {
+            nz = *reinterpret_cast<const float2*>(e.noise + n * e.noise_nstride + pix);
+            nz.x *= nstr;
+            nz.y *= nstr;
+        }
+        *reinterpret_cast<float2*>(y + plane + pix) =
+            make_float2(smc::epi_y(u2.x, dv, nz.x, bv, e.act, e.alpha, e.gain, e.clamp),
+                        smc::epi_y(u2.y, dv, nz.y, bv, e.act, e.alpha, e.gain, e.clamp));
+    }
+}
+
 // Backward of conv0's epilogue + FIR in one pass: du = act'(g; y(u)) * d (re-derived per element of the
 // haloed tile), dT = FIR^T(du) (pad (pady0, padx0) of the adjoint), dd[n,o] += sum dz*u over the du
 // positions this tile owns (its own 32x64 window, so every position is counted exactly once).
 template <int FH, int FW, bool V2 = false>
 __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const float* u, float* dt, float* dd, int c,
-                                                         int u_h, int u_w, int t_h, int t_w, const float* f, int padx0,
+                                                         int u_h, int u_w, int t_h, int t_w, int tp_w, const float* f,
+                                                         int padx0,
                                                          int pady0, float fgain, int flip, Epi e) {
     constexpr int ROWS = kFH + FH - 1, COLS = kFW + FW - 1, STRIDE = COLS + 1;
     __shared__ __attribute__((aligned(16))) float tile[ROWS * STRIDE];
@@ -395,7 +485,7 @@ __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const f
     __syncthreads();
     float out[4][2];
     fir_block_split<FH, FW>(tile, STRIDE, 4 * ty, tx, tp, out);
-    const int64_t tplane = nc * (int64_t)t_h * t_w;
+    const int64_t tplane = nc * (int64_t)t_h * tp_w;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int oy = oy0 + 4 * ty + i;
@@ -403,7 +493,90 @@ __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const f
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int ox = ox0 + tx + 32 * j;
-            if (ox < t_w) dt[tplane + (int64_t)oy * t_w + ox] = out[i][j];
+            if (ox < t_w) dt[tplane + (int64_t)oy * tp_w + ox] = out[i][j];
+        }
+    }
+    if (dd) {
+        const float tot = block_sum256(part, red);
+        if (tid == 0) atomicAdd(dd + nc, tot);
+    }
+}
+
+// blur_act_bwd_fast with 16-B loads of u / g / noise (u_w % 4 == 0, 16-B aligned planes): aligned float4 groups
+// covering [ox0 - 4, ox0 + kFW + 4), elements outside the tile window dropped, outside the image zeroed.
+template <int FH, int FW>
+__global__ __launch_bounds__(256) void blur_act_bwd_v4(const float* g, const float* u, float* dt, float* dd, int c,
+                                                       int u_h, int u_w, int t_h, int t_w, int tp_w, const float* f,
+                                                       int padx0, int pady0, float fgain, int flip, Epi e) {
+    constexpr int ROWS = kFH + FH - 1, COLS = kFW + FW - 1, STRIDE = COLS + 1;
+    constexpr int G4 = (kFW + 8) / 4;
+    constexpr int NL = (ROWS * G4 + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float tile[ROWS * STRIDE];
+    __shared__ float red[4];
+    const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
+    const int ox0 = blockIdx.x * kFW, oy0 = blockIdx.y * kFH;
+    const int64_t nc = blockIdx.z;
+    const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
+    float tp[FH][FW];
+    load_taps<FH, FW>(f, flip, fgain, tp);
+    const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
+    const float dv = e.d ? e.d[nc] : 1.f;
+    const float bv = e.bias ? e.bias[o] : 0.f;
+    const int iy0 = oy0 - pady0, ix0 = ox0 - padx0;
+    const int64_t uplane = nc * (int64_t)u_h * u_w;
+    const float* up = u + uplane;
+    const float* gp = g + uplane;
+    const float* np_ = e.noise ? e.noise + n * e.noise_nstride : nullptr;
+    float part = 0.f;
+    float4 uv[NL], gv[NL], nv[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        const int i = tid + 256 * l;
+        const int r = i / G4, q = i - r * G4;
+        const int iy = iy0 + r, x = ox0 - 4 + 4 * q;
+        const bool ok = i < ROWS * G4 && iy >= 0 && iy < u_h && x >= 0 && x < u_w;
+        const int pix = ok ? iy * u_w + x : 0;
+        uv[l] = *reinterpret_cast<const float4*>(up + pix);
+        gv[l] = *reinterpret_cast<const float4*>(gp + pix);
+        nv[l] = np_ ? *reinterpret_cast<const float4*>(np_ + pix) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        const int i = tid + 256 * l;
+        if (i >= ROWS * G4) continue;
+        const int r = i / G4, q = i - r * G4;
+        const int iy = iy0 + r, x = ox0 - 4 + 4 * q;
+        const bool rok = iy >= 0 && iy < u_h;
+        const float ua[4] = {uv[l].x, uv[l].y, uv[l].z, uv[l].w};
+        const float ga[4] = {gv[l].x, gv[l].y, gv[l].z, gv[l].w};
+        const float na[4] = {nv[l].x, nv[l].y, nv[l].z, nv[l].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int ix = x + k;
+            const int cc = ix - ix0;
+            if (cc < 0 || cc >= COLS) continue;
+            float val = 0.f;
+            if (rok && ix >= 0 && ix < u_w) {
+                const float yv = smc::epi_y(ua[k], dv, na[k] * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
+                const float dz = smc::act_grad_y(e.act, ga[k], yv, e.alpha, e.gain, e.clamp);
+                if (iy >= oy0 && iy < oy0 + kFH && ix >= ox0 && ix < ox0 + kFW) part += dz * ua[k];
+                val = dz * dv;
+            }
+            tile[r * STRIDE + cc] = val;
+        }
+    }
+    __syncthreads();
+    float out[4][2];
+    fir_block_split<FH, FW>(tile, STRIDE, 4 * ty, tx, tp, out);
+    const int64_t tplane = nc * (int64_t)t_h * tp_w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int oy = oy0 + 4 * ty + i;
+        if (oy >= t_h) continue;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int ox = ox0 + tx + 32 * j;
+            if (ox < t_w) dt[tplane + (int64_t)oy * tp_w + ox] = out[i][j];
         }
     }
     if (dd) {
@@ -525,6 +698,41 @@ __global__ __launch_bounds__(256) void channel_dot_kernel(const float* a, const 
     if (threadIdx.x == 0) out[r] = accumulate ? out[r] + tot : tot;
 }
 
+// 16-B form for aligned rows with len % 4 == 0: four float4 pairs in flight per thread per trip (the scalar form keeps
+// one 4-B load pair in flight and reaches ~0.6 TB/s on the 128 rows x 1 M of the r = 1024 layer).
+__global__ __launch_bounds__(256) void channel_dot_v4_kernel(const float4* a, const float4* b, const float* scale,
+                                                             float* out, float4* a_scaled, int64_t len4,
+                                                             int accumulate) {
+    __shared__ float red[4];
+    const int64_t r = blockIdx.x;
+    const float4* ap = a + r * len4;
+    const float4* bp = b + r * len4;
+    float4* sp = a_scaled ? a_scaled + r * len4 : nullptr;
+    const float sc = scale ? scale[r] : 1.f;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t p = threadIdx.x;
+    for (; p + 768 < len4; p += 1024) {
+        float4 av[4], bv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            av[k] = ap[p + 256 * k];
+            bv[k] = bp[p + 256 * k];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            acc[k] += av[k].x * bv[k].x + av[k].y * bv[k].y + av[k].z * bv[k].z + av[k].w * bv[k].w;
+            if (sp) sp[p + 256 * k] = make_float4(av[k].x * sc, av[k].y * sc, av[k].z * sc, av[k].w * sc);
+        }
+    }
+    for (; p < len4; p += 256) {
+        const float4 av = ap[p], bv = bp[p];
+        acc[0] += av.x * bv.x + av.y * bv.y + av.z * bv.z + av.w * bv.w;
+        if (sp) sp[p] = make_float4(av.x * sc, av.y * sc, av.z * sc, av.w * sc);
+    }
+    const float tot = block_sum256((acc[0] + acc[1]) + (acc[2] + acc[3]), red);
+    if (threadIdx.x == 0) out[r] = accumulate ? out[r] + tot : tot;
+}
+
 // ---------------------------------------------------------------------------------------------- demod bwd
 
 // 32 input channels x 8 output-channel groups per workgroup; each thread sums a strided slice of o
@@ -574,25 +782,36 @@ SMC_API int smc_modconv_epilogue_f32(const float* src, int nsplit, int64_t split
 }
 
 SMC_API int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_stride, float* y, int n, int c,
-                                     int t_h, int t_w, int y_h, int y_w, const float* f, int fh, int fw, int padx0,
-                                     int pady0, float fgain, int flip, const smc_conv_epilogue* epi, void* stream) {
+                                     int t_h, int t_w, int t_pitch, int y_h, int y_w, const float* f, int fh, int fw,
+                                     int padx0, int pady0, float fgain, int flip, const smc_conv_epilogue* epi,
+                                     void* stream) {
     SMC_CHECK(t && y && f && n >= 1 && c >= 1 && nsplit >= 1, "smc_modconv_blur_act_f32: bad args");
     if (fh > kMaxF || fw > kMaxF || fh < 1 || fw < 1) {
         smc::set_error("smc_modconv_blur_act_f32: filter %dx%d > %dx%d", fh, fw, kMaxF, kMaxF);
         return SMC_ERR_UNSUPPORTED;
     }
+    const int tp_w = t_pitch > 0 ? t_pitch : t_w;
+    SMC_CHECK(tp_w >= t_w, "smc_modconv_blur_act_f32: t_pitch < t_w");
     SMC_CHECK(y_h >= 1 && y_w >= 1 && y_h <= t_h + 2 * pady0 && y_w <= t_w + 2 * padx0,
               "smc_modconv_blur_act_f32: bad output size");
     SMC_CHECK((int64_t)n * c < 65536, "smc_modconv_blur_act_f32: too many planes");
+    hipStream_t st = smc::as_stream(stream);
     if (fh == 4 && fw == 4) {
         dim3 grid((unsigned)smc::ceil_div(y_w, kFW), (unsigned)smc::ceil_div(y_h, kFH), (unsigned)(n * c));
-        hipLaunchKernelGGL((blur_act_fast<4, 4>), grid, dim3(256), 0, smc::as_stream(stream), t, nsplit, split_stride,
-                           y, c, t_h, t_w, y_h, y_w, f, padx0, pady0, fgain, flip, to_epi(epi));
+        const uintptr_t al = (uintptr_t)t | (uintptr_t)y | (uintptr_t)epi->u_save | (uintptr_t)epi->noise;
+        const bool v4 = split_stride % 4 == 0 && (al & 15) == 0 && y_w % 2 == 0 &&
+                        epi->noise_nstride % 2 == 0 && padx0 <= 4 && fw - 1 - padx0 <= 4;
+        if (v4)
+            hipLaunchKernelGGL((blur_act_v4<4, 4>), grid, dim3(256), 0, st, t, nsplit, split_stride, y, c, t_h, t_w, tp_w,
+                               y_h, y_w, f, padx0, pady0, fgain, flip, to_epi(epi));
+        else
+            hipLaunchKernelGGL((blur_act_fast<4, 4>), grid, dim3(256), 0, st, t, nsplit, split_stride, y, c, t_h, t_w,
+                               tp_w, y_h, y_w, f, padx0, pady0, fgain, flip, to_epi(epi));
         return smc::check_launch("smc_modconv_blur_act_f32");
     }
     dim3 grid((unsigned)smc::ceil_div(y_w, kBT), (unsigned)smc::ceil_div(y_h, kBT), (unsigned)(n * c));
-    hipLaunchKernelGGL(blur_act_kernel, grid, dim3(256), 0, smc::as_stream(stream), t, nsplit, split_stride, y, c,
-                       t_h, t_w, y_h, y_w, f, fh, fw, padx0, pady0, fgain, flip, to_epi(epi));
+    hipLaunchKernelGGL(blur_act_kernel, grid, dim3(256), 0, st, t, nsplit, split_stride, y, c, t_h, t_w, tp_w, y_h, y_w,
+                       f, fh, fw, padx0, pady0, fgain, flip, to_epi(epi));
     return smc::check_launch("smc_modconv_blur_act_f32");
 }
 
@@ -631,6 +850,12 @@ SMC_API int smc_channel_dot_f32(const float* a, const float* b, const float* sca
     SMC_CHECK(a && b && out && rows >= 1 && len >= 1, "smc_channel_dot_f32: bad args");
     SMC_CHECK(!a_scaled || scale, "smc_channel_dot_f32: a_scaled needs scale");
     SMC_CHECK(rows < (1LL << 31), "smc_channel_dot_f32: too many rows");
+    if (len % 4 == 0 && (((uintptr_t)a | (uintptr_t)b | (uintptr_t)a_scaled) & 15) == 0) {
+        hipLaunchKernelGGL(channel_dot_v4_kernel, dim3((unsigned)rows), dim3(256), 0, smc::as_stream(stream),
+                           reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(b), scale, out,
+                           reinterpret_cast<float4*>(a_scaled), len / 4, accumulate);
+        return smc::check_launch("smc_channel_dot_f32");
+    }
     hipLaunchKernelGGL(channel_dot_kernel, dim3((unsigned)rows), dim3(256), 0, smc::as_stream(stream), a, b, scale,
                        out, a_scaled, len, accumulate);
     return smc::check_launch("smc_channel_dot_f32");
@@ -646,26 +871,34 @@ SMC_API int smc_modconv_demod_bwd_f32(const float* s, const float* d, const floa
 }
 
 SMC_API int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* dt, float* dd, int n, int c, int u_h,
-                                         int u_w, int t_h, int t_w, const float* f, int fh, int fw, int padx0,
-                                         int pady0, float fgain, int flip, const smc_conv_epilogue* epi,
+                                         int u_w, int t_h, int t_w, int t_pitch, const float* f, int fh, int fw,
+                                         int padx0, int pady0, float fgain, int flip, const smc_conv_epilogue* epi,
                                          void* stream) {
     SMC_CHECK(g && u && dt && f && n >= 1 && c >= 1 && u_h >= 1 && u_w >= 1, "smc_modconv_blur_act_bwd_f32: bad args");
     SMC_CHECK(epi && epi->mode == SMC_EPI_MODACT, "smc_modconv_blur_act_bwd_f32: needs a MODACT epilogue");
     SMC_CHECK(t_h == u_h + 2 * pady0 - fh + 1 && t_w == u_w + 2 * padx0 - fw + 1,
               "smc_modconv_blur_act_bwd_f32: t shape does not match the adjoint FIR");
+    const int tp_w = t_pitch > 0 ? t_pitch : t_w;
+    SMC_CHECK(tp_w >= t_w, "smc_modconv_blur_act_bwd_f32: t_pitch < t_w");
     SMC_CHECK((int64_t)n * c < 65536, "smc_modconv_blur_act_bwd_f32: too many planes");
     if (fh != 4 || fw != 4) {
         smc::set_error("smc_modconv_blur_act_bwd_f32: only the 4x4 FIR has a fused kernel (got %dx%d)", fh, fw);
         return SMC_ERR_UNSUPPORTED;
     }
+    hipStream_t st = smc::as_stream(stream);
     dim3 grid((unsigned)smc::ceil_div(t_w, kFW), (unsigned)smc::ceil_div(t_h, kFH), (unsigned)(n * c));
-    const bool v2 = u_w % 2 == 0 && padx0 % 2 == 0 && epi->noise_nstride % 2 == 0 &&
-                    (((uintptr_t)g | (uintptr_t)u | (uintptr_t)epi->noise) & 7) == 0;
+    const uintptr_t al = (uintptr_t)g | (uintptr_t)u | (uintptr_t)epi->noise;
+    if (u_w % 4 == 0 && epi->noise_nstride % 4 == 0 && (al & 15) == 0 && padx0 <= 4 && fw - 1 - padx0 <= 4) {
+        hipLaunchKernelGGL((blur_act_bwd_v4<4, 4>), grid, dim3(256), 0, st, g, u, dt, dd, c, u_h, u_w, t_h, t_w, tp_w, f,
+                           padx0, pady0, fgain, flip, to_epi(epi));
+        return smc::check_launch("smc_modconv_blur_act_bwd_f32");
+    }
+    const bool v2 = u_w % 2 == 0 && padx0 % 2 == 0 && epi->noise_nstride % 2 == 0 && ((al & 7) == 0);
     if (v2)
-        hipLaunchKernelGGL((blur_act_bwd_fast<4, 4, true>), grid, dim3(256), 0, smc::as_stream(stream), g, u, dt, dd, c,
-                           u_h, u_w, t_h, t_w, f, padx0, pady0, fgain, flip, to_epi(epi));
+        hipLaunchKernelGGL((blur_act_bwd_fast<4, 4, true>), grid, dim3(256), 0, st, g, u, dt, dd, c, u_h, u_w, t_h, t_w,
+                           tp_w, f, padx0, pady0, fgain, flip, to_epi(epi));
     else
-        hipLaunchKernelGGL((blur_act_bwd_fast<4, 4>), grid, dim3(256), 0, smc::as_stream(stream), g, u, dt, dd, c, u_h,
-                           u_w, t_h, t_w, f, padx0, pady0, fgain, flip, to_epi(epi));
+        hipLaunchKernelGGL((blur_act_bwd_fast<4, 4>), grid, dim3(256), 0, st, g, u, dt, dd, c, u_h, u_w, t_h, t_w, tp_w,
+                           f, padx0, pady0, fgain, flip, to_epi(epi));
     return smc::check_launch("smc_modconv_blur_act_bwd_f32");
 }

@@ -178,7 +178,7 @@ class ModConvFn(torch.autograd.Function):
                  alg_flops=conv_flops(n, cin, P.cout, h, w, 9), alg_bytes=4 * x.numel() + 4 * t.numel() + wbytes)
             f = spec.filter.to(x.device)
             fh, fw = f.shape
-            _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, P.cout, th, tw, r_h, r_w,
+            _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, P.cout, th, tw, 0, r_h, r_w,
                       _hip.ptr(f), fh, fw, 1, 1, 4.0, 0, ctypes.byref(epi), _hip.stream())
         ctx.spec, ctx.gain, ctx.clamp = spec, gain, clamp
         ctx.noise, ctx.nstride, ctx.strength = nz, nstride, strength
@@ -206,10 +206,13 @@ class ModConvFn(torch.autograd.Function):
             # fused: epilogue backward + adjoint of FIR(pad 1, gain 4) (pad fw-1-1 = 2, correlation) + dd
             f = spec.filter.to(x.device)
             fh, fw = f.shape
+            # dT rows padded to a multiple of 4 floats (aligned 16-B row starts for the FIR's stores and the gather
+            # GEMM's loads); the stride-2 gather reads columns <= 2w only, so the pad columns are never read.
             th, tw = 2 * h + 1, 2 * w + 1
-            g = torch.empty(n, P.cout, th, tw, device=x.device, dtype=torch.float32)
+            pitch = (tw + 3) // 4 * 4
+            g = torch.empty(n, P.cout, th, pitch, device=x.device, dtype=torch.float32)
             _hip.call("smc_modconv_blur_act_bwd_f32", gy.data_ptr(), u.data_ptr(), g.data_ptr(), _hip.ptr(dd), n,
-                      P.cout, u.shape[2], u.shape[3], th, tw, _hip.ptr(f), fh, fw, fw - 2, fh - 2, 4.0, 1,
+                      P.cout, u.shape[2], u.shape[3], th, tw, pitch, _hip.ptr(f), fh, fw, fw - 2, fh - 2, 4.0, 1,
                       ctypes.byref(epi), _hip.stream())
         dx = torch.empty_like(x) if need_dx else None
         dxs = torch.empty_like(x) if need_ds else None
@@ -220,8 +223,9 @@ class ModConvFn(torch.autograd.Function):
             ebw = _epilogue(_hip.EPI_STORE)
             out = dxs
         phases, nph = P.bwd_phases(h, w)
+        g_bytes = 4 * g.numel() if spec.up == 1 else 4 * n * P.cout * (2 * h + 1) * (2 * w + 1)
         gemm(g, out, phases, nph, P.cout, cin, epi=ebw, alg_flops=conv_flops(n, P.cout, cin, h, w, P.k * P.k),
-             alg_bytes=4 * g.numel() + 4 * out.numel() * (2 if (need_dx and need_ds) else 1) + 4 * P.k * P.k * cin * P.cout)
+             alg_bytes=g_bytes + 4 * out.numel() * (2 if (need_dx and need_ds) else 1) + 4 * P.k * P.k * cin * P.cout)
         ds = None
         if need_ds:
             ds = torch.empty(n, cin, device=x.device, dtype=torch.float32)

@@ -284,6 +284,73 @@ def test_conv_gemm_transposed_vs_conv_transpose2d(n, cin, cout, h):
     close(t, ref, 2e-5, "transposed conv")
 
 
+def _misaligned(t):
+    """A copy of `t` whose data pointer is 4 B past a 16-B boundary (forces the scalar-load kernels)."""
+    buf = torch.empty(t.numel() + 1, device=t.device, dtype=t.dtype)
+    v = buf[1:].view(t.shape)
+    v.copy_(t)
+    assert v.data_ptr() % 16 == 4
+    return v
+
+
+@pytest.mark.parametrize("n,c,h", [(2, 8, 64), (1, 4, 37), (2, 3, 256)])
+def test_blur_act_load_paths(n, c, h):
+    """conv0's fused FIR + modconv epilogue (smc_modconv_blur_act_f32) and its backward: the 16-B load kernels
+    (16-B aligned buffers; any T row pitch, incl. the transposed conv's odd 2h + 1 and an explicit padded pitch)
+    against the scalar-load kernels (a misaligned copy of the same buffers) -- the same FIR arithmetic, so y, u and
+    dT must agree bit for bit (dd: block sums in a different atomic order, 1e-6) -- and U against fp64 torch."""
+    import ctypes
+    import torch.nn.functional as F
+    from stylemc_amd import _hip, modconv
+    gen = torch.Generator().manual_seed(21)
+    th, r = 2 * h + 1, 2 * h
+    f1 = torch.tensor([1.0, 3.0, 3.0, 1.0])
+    f = (f1[:, None] * f1[None, :] / 64.0).to(DEV)
+    T = torch.randn(n, c, th, th, generator=gen).to(DEV)
+    d = (torch.rand(n, c, generator=gen) + 0.5).to(DEV)
+    noise = torch.randn(r, r, generator=gen).to(DEV)
+    strength = torch.tensor(0.3, device=DEV)
+    bias = (torch.randn(c, generator=gen) * 0.1).to(DEV)
+    st = _hip.stream()
+
+    def fwd(tbuf, pitch):
+        y = torch.empty(n, c, r, r, device=DEV)
+        u = torch.empty_like(y)
+        epi = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 1.0, u)
+        _hip.call("smc_modconv_blur_act_f32", tbuf.data_ptr(), 1, 0, y.data_ptr(), n, c, th, th, pitch, r, r,
+                  f.data_ptr(), 4, 4, 1, 1, 4.0, 0, ctypes.byref(epi), st)
+        return y, u
+
+    y0, u0 = fwd(T, 0)
+    Tp = torch.zeros(n, c, th, th + 7, device=DEV)
+    Tp[..., :th] = T
+    y1, u1 = fwd(Tp, th + 7)
+    y2, u2 = fwd(_misaligned(T), 0)
+    torch.cuda.synchronize()
+    for a, b, what in ((y1, y0, "y pitched"), (u1, u0, "u pitched"), (y2, y0, "y scalar"), (u2, u0, "u scalar")):
+        assert torch.equal(a, b), what
+    ref = F.conv2d(F.pad(T.double().cpu(), (1, 1, 1, 1)).view(n * c, 1, th + 2, th + 2),
+                   (4.0 * f.double().cpu().flip(0, 1))[None, None]).view(n, c, r, r)
+    close(u0, ref, 2e-6, "U vs fp64")
+
+    g = torch.randn(n, c, r, r, generator=gen).to(DEV)
+
+    def bwd(gb, ub):
+        dt = torch.full((n, c, th, th), float("nan"), device=DEV)
+        dd = torch.zeros(n, c, device=DEV)
+        epi = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 1.0)
+        _hip.call("smc_modconv_blur_act_bwd_f32", gb.data_ptr(), ub.data_ptr(), dt.data_ptr(), dd.data_ptr(), n, c,
+                  r, r, th, th, 0, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epi), st)
+        return dt, dd
+
+    dt0, dd0 = bwd(g, u0)
+    dt1, dd1 = bwd(_misaligned(g), _misaligned(u0))
+    torch.cuda.synchronize()
+    assert torch.isfinite(dt0).all()
+    assert torch.equal(dt0, dt1), "dT scalar vs 16-B loads"
+    close(dd0, dd1, 1e-6, "dd")
+
+
 def test_conv_gemm_2gib_input_fallback():
     """An input of >= 2 GiB (batch 16 of the r = 1024 conv1: 2.1 GB) exceeds the 32-bit buffer offsets of the
     LDS-DMA / row-halo kernels and runs the register-staged kernel with 64-bit addressing: it must equal the

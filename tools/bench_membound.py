@@ -53,7 +53,7 @@ def main():
         st = _hip.stream()
 
         def blur():
-            _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, c, th, th, r, r, f.data_ptr(),
+            _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, c, th, th, 0, r, r, f.data_ptr(),
                       4, 4, 1, 1, 4.0, 0, ctypes.byref(epi), st)
         us = timeit(blur)
         byt = 4 * (t.numel() + 2 * y.numel())
@@ -65,10 +65,18 @@ def main():
 
         def blur_b():
             _hip.call("smc_modconv_blur_act_bwd_f32", g.data_ptr(), u.data_ptr(), dt.data_ptr(), dd.data_ptr(), n, c,
-                      r, r, th, th, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epib), st)
+                      r, r, th, th, 0, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epib), st)
         us = timeit(blur_b)
         byt = 4 * (2 * y.numel() + t.numel())
         print(f"r={r:5d} c={c:4d} blur_act_bwd  {us:8.1f} us  {byt / us / 1e3:7.0f} GB/s")
+        tp = (th + 3) // 4 * 4
+        dtp = torch.empty(n, c, th, tp, device=dev)
+
+        def blur_bp():
+            _hip.call("smc_modconv_blur_act_bwd_f32", g.data_ptr(), u.data_ptr(), dtp.data_ptr(), dd.data_ptr(), n, c,
+                      r, r, th, th, tp, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epib), st)
+        us = timeit(blur_bp)
+        print(f"r={r:5d} c={c:4d} blur_act_bwd_pitch{tp} {us:8.1f} us  {byt / us / 1e3:7.0f} GB/s")
         du = torch.empty_like(y)
 
         def actb():
