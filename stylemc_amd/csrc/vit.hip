@@ -221,7 +221,8 @@ int lin_nsplit(int M, int N, int K) {
     return best;
 }
 
-int64_t lin_tiles(int M, int N) { return smc::ceil_div(M, LBM) * smc::ceil_div(N, LBN); }
+// output tiles of a call (the in-launch split-K counters): the v2 kernel's 32 x 64 tiles, >= the v1 kernel's 32 x 128
+int64_t lin_tiles(int M, int N) { return smc::ceil_div(M, 32) * smc::ceil_div(N, 64); }
 
 int64_t lin_ws_floats(int M, int N, int K);  // defined after the v2 kernel (same plan as lin_launch)
 
@@ -344,10 +345,56 @@ __global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, 
         for (int rr = 0; rr < 4; ++rr) {
             const int m = m0 + wm * 16 + 4 * g + rr;
             if (m >= p.M) continue;
-            if (p.nsplit > 1)
-                p.ws[((int64_t)split * p.M + m) * p.N + n] = acc[blk][rr];
-            else
+            if (p.nsplit == 1)
                 p.c[(int64_t)m * p.ldc + n] = lin_epi(acc[blk][rr], m, n, p.e);
+            else if (p.counters)  // write-through (sc1): the hand-off below needs no release fence
+                __hip_atomic_store(p.ws + ((int64_t)split * p.M + m) * p.N + n, acc[blk][rr], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            else
+                p.ws[((int64_t)split * p.M + m) * p.N + n] = acc[blk][rr];
+        }
+    }
+    if (p.nsplit == 1 || !p.counters) return;
+    // In-launch split-K hand-off (cdna_hip_programming.md section 6 Guideline 16, R1 counter form): every wave drains
+    // its write-through partial stores, one lane takes a ticket, the last split's workgroup acquires and sums the
+    // partials in split order (the separate epilogue kernel's order).  Measured (profiles/r02_splitk_inlaunch_ab):
+    // ViT-B/32 B = 8 fwd + bwd 4.7-5.0 -> 3.7 ms, no-grad fwd 1.60 -> 1.70 ms; the same hand-off in the synthesis /
+    // IR-SE50 conv GEMM lost (layer set 10.75 -> 11.7 ms), so that one keeps its reduction kernel.
+    int* flag = reinterpret_cast<int*>(smem);  // the k-loop is over: the LDS array is free
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const int prev = __hip_atomic_fetch_add(p.counters + n_tile * mt + m_tile, 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == p.nsplit - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    // split-major sums: all 8 loads of one split in flight before the adds; rows past M re-read row M - 1
+    float v[2][4];
+    for (int k = 0; k < p.nsplit; ++k) {
+        const float* part = p.ws + (int64_t)k * p.M * p.N;
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int m = min(m0 + wm * 16 + 4 * g + rr, p.M - 1);
+                const float t = part[(int64_t)m * p.N + n0 + wn * 32 + blk * 16 + i];
+                v[blk][rr] = k == 0 ? t : v[blk][rr] + t;
+            }
+    }
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+        const int n = n0 + wn * 32 + blk * 16 + i;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int m = m0 + wm * 16 + 4 * g + rr;
+            if (m < p.M) p.c[(int64_t)m * p.ldc + n] = lin_epi(v[blk][rr], m, n, p.e);
         }
     }
 }
@@ -392,7 +439,7 @@ int lin_launch(const float* a, int lda, const float* b, int ldb, float* c, int l
         SMC_CHECK(ws && ws_bytes >= need, "smc_linear_f32: workspace %lld < %lld bytes", (long long)ws_bytes,
                   (long long)need);
         p.ws = ws;
-        p.counters = v2 ? nullptr : counters;
+        p.counters = counters;
     }
     if (v2) {
         const int mt = (int)smc::ceil_div(M, L2M), ntl = N / L2N;
@@ -1092,8 +1139,7 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
             smc::set_error("smc_vit: split-K counter slices exhausted");
             return SMC_ERR_INVALID;
         }
-        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st,
-                          nullptr);
+        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr);
     };
     if (hipMemsetAsync(ws.counters, 0, sizeof(int) * (size_t)ws.counter_ints, st) != hipSuccess) {
         smc::set_error("smc_vit: counter memset failed");
@@ -1183,8 +1229,7 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
             smc::set_error("smc_vit: split-K counter slices exhausted");
             return SMC_ERR_INVALID;
         }
-        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st,
-                          nullptr);
+        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr);
     };
     if (hipMemsetAsync(ws.counters, 0, sizeof(int) * (size_t)ws.counter_ints, st) != hipSuccess) {
         smc::set_error("smc_vit: counter memset failed");
