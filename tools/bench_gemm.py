@@ -29,12 +29,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default="", help="comma-separated name filters, e.g. fwd_conv0 or fwd_conv0:128")
     args = ap.parse_args()
+    only = [f for f in args.only.split(",") if f]
     build.build(verbose=False)
     dev = "cuda"
     n = args.batch
     tot_f = tot_t = 0.0
     for name, r, cin, cout, up, kind in shapes(n):
+        if only and not any(f == name or f == f"{name}:{r}" for f in only):
+            continue
         W = torch.randn(cout, cin, 3, 3, device=dev)
         P = modconv.PackedConv(W, up)
         h = r // up
