@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 1
+#define SMC_ABI_VERSION 2
 
 #define SMC_OK 0
 #define SMC_ERR_INVALID 1     /* bad argument / shape (reference: TORCH_CHECK -> RuntimeError)   */
@@ -114,6 +114,10 @@ typedef struct {
     const float* act_ref;          /* PRELU_GRAD: the saved pre-activation, layout of y             */
     const float* residual;         /* may be NULL: added last, [n][cout][y_h/rs][y_w/rs] at the      */
     int residual_stride;           /*   positions with y % rs == 0 and x % rs == 0 (rs 0 -> 1)      */
+    int grad_from_y;               /* MODACT backward entry points (act_bwd, blur_act_bwd): their `u`
+                                    * argument holds the forward OUTPUT y instead of u -- the
+                                    * activation mask needs only y, so a layer whose styles need no
+                                    * gradient saves no u -- and dd must be NULL (it needs u)         */
 } smc_conv_epilogue;
 
 /* bytes of workspace smc_conv_gemm_f32 needs for these sizes (0 = none). */

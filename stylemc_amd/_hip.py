@@ -30,7 +30,8 @@ class ConvEpilogue(ctypes.Structure):
     _fields_ = [("mode", c_int), ("d", c_void_p), ("noise", c_void_p), ("noise_nstride", c_int64),
                 ("noise_strength", c_void_p), ("bias", c_void_p), ("act", c_int), ("alpha", c_float),
                 ("gain", c_float), ("clamp", c_float), ("u_save", c_void_p), ("scale_c", c_void_p),
-                ("alpha_c", c_void_p), ("act_ref", c_void_p), ("residual", c_void_p), ("residual_stride", c_int)]
+                ("alpha_c", c_void_p), ("act_ref", c_void_p), ("residual", c_void_p), ("residual_stride", c_int),
+                ("grad_from_y", c_int)]
 
 
 class LinearEpilogue(ctypes.Structure):
@@ -114,7 +115,7 @@ def load(path=None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.smc_abi_version() != 1:
+        if lib.smc_abi_version() != 2:
             raise RuntimeError("stylemc_amd: ABI version mismatch, rebuild the library")
         if path is None:
             _lib = lib

@@ -23,6 +23,7 @@ struct Epi {
     float alpha, gain, clamp;
     float* u_save;
     smc::EpiExt ext;
+    int grad_from_y;
 };
 
 Epi to_epi(const smc_conv_epilogue* e) {
@@ -34,7 +35,7 @@ Epi to_epi(const smc_conv_epilogue* e) {
     if (e) {
         r.mode = e->mode; r.d = e->d; r.noise = e->noise; r.noise_nstride = e->noise_nstride;
         r.noise_strength = e->noise_strength; r.bias = e->bias; r.act = e->act; r.alpha = e->alpha;
-        r.gain = e->gain; r.clamp = e->clamp; r.u_save = e->u_save;
+        r.gain = e->gain; r.clamp = e->clamp; r.u_save = e->u_save; r.grad_from_y = e->grad_from_y;
     }
     r.ext = smc::epi_ext(e);
     return r;
@@ -399,7 +400,8 @@ __global__ __launch_bounds__(256) void blur_act_v4(const float* t, int nsplit, i
 // Backward of conv0's epilogue + FIR in one pass: du = act'(g; y(u)) * d (re-derived per element of the
 // haloed tile), dT = FIR^T(du) (pad (pady0, padx0) of the adjoint), dd[n,o] += sum dz*u over the du
 // positions this tile owns (its own 32x64 window, so every position is counted exactly once).
-template <int FH, int FW, bool V2 = false>
+// FROMY (epi.grad_from_y): `u` holds the forward output y -- the mask needs nothing else; no noise read, no dd.
+template <int FH, int FW, bool V2 = false, bool FROMY = false>
 __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const float* u, float* dt, float* dd, int c,
                                                          int u_h, int u_w, int t_h, int t_w, int tp_w, const float* f,
                                                          int padx0,
@@ -422,8 +424,9 @@ __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const f
     // fixed-trip unrolled loads (u, g, noise of every element in flight at once), then the math
     const float* up = u + uplane;
     const float* gp = g + uplane;
-    const float* np_ = e.noise ? e.noise + n * e.noise_nstride : nullptr;
+    const float* np_ = !FROMY && e.noise ? e.noise + n * e.noise_nstride : nullptr;
     auto elem = [&](float uu, float gg, float nn, int iy, int ix) {
+        if constexpr (FROMY) return smc::act_grad_y(e.act, gg, uu, e.alpha, e.gain, e.clamp) * dv;
         const float yv = smc::epi_y(uu, dv, nn * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
         const float dz = smc::act_grad_y(e.act, gg, yv, e.alpha, e.gain, e.clamp);
         if (iy >= oy0 && iy < oy0 + kFH && ix >= ox0 && ix < ox0 + kFW) part += dz * uu;
@@ -504,7 +507,7 @@ __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const f
 
 // blur_act_bwd_fast with 16-B loads of u / g / noise (u_w % 4 == 0, 16-B aligned planes): aligned float4 groups
 // covering [ox0 - 4, ox0 + kFW + 4), elements outside the tile window dropped, outside the image zeroed.
-template <int FH, int FW>
+template <int FH, int FW, bool FROMY = false>
 __global__ __launch_bounds__(256) void blur_act_bwd_v4(const float* g, const float* u, float* dt, float* dd, int c,
                                                        int u_h, int u_w, int t_h, int t_w, int tp_w, const float* f,
                                                        int padx0, int pady0, float fgain, int flip, Epi e) {
@@ -526,7 +529,7 @@ __global__ __launch_bounds__(256) void blur_act_bwd_v4(const float* g, const flo
     const int64_t uplane = nc * (int64_t)u_h * u_w;
     const float* up = u + uplane;
     const float* gp = g + uplane;
-    const float* np_ = e.noise ? e.noise + n * e.noise_nstride : nullptr;
+    const float* np_ = !FROMY && e.noise ? e.noise + n * e.noise_nstride : nullptr;
     float part = 0.f;
     float4 uv[NL], gv[NL], nv[NL];
 #pragma unroll
@@ -557,10 +560,14 @@ __global__ __launch_bounds__(256) void blur_act_bwd_v4(const float* g, const flo
             if (cc < 0 || cc >= COLS) continue;
             float val = 0.f;
             if (rok && ix >= 0 && ix < u_w) {
-                const float yv = smc::epi_y(ua[k], dv, na[k] * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
-                const float dz = smc::act_grad_y(e.act, ga[k], yv, e.alpha, e.gain, e.clamp);
-                if (iy >= oy0 && iy < oy0 + kFH && ix >= ox0 && ix < ox0 + kFW) part += dz * ua[k];
-                val = dz * dv;
+                if constexpr (FROMY) {
+                    val = smc::act_grad_y(e.act, ga[k], ua[k], e.alpha, e.gain, e.clamp) * dv;
+                } else {
+                    const float yv = smc::epi_y(ua[k], dv, na[k] * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
+                    const float dz = smc::act_grad_y(e.act, ga[k], yv, e.alpha, e.gain, e.clamp);
+                    if (iy >= oy0 && iy < oy0 + kFH && ix >= ox0 && ix < ox0 + kFW) part += dz * ua[k];
+                    val = dz * dv;
+                }
             }
             tile[r * STRIDE + cc] = val;
         }
@@ -606,6 +613,7 @@ __global__ __launch_bounds__(256) void demod_kernel(const float* s, const float*
 
 // ---------------------------------------------------------------------------------------------- act bwd
 
+template <bool FROMY>
 __global__ __launch_bounds__(256) void act_bwd_kernel(const float* g, const float* u, float* du, float* dd, int c,
                                                       int64_t hw, Epi e) {
     __shared__ float red[4];
@@ -618,6 +626,10 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const float* g, const floa
     float part = 0.f;
     for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < hw; p += (int64_t)gridDim.x * 256) {
         const float uv = u[base + p];
+        if constexpr (FROMY) {
+            du[base + p] = smc::act_grad_y(e.act, g[base + p], uv, e.alpha, e.gain, e.clamp) * dv;
+            continue;
+        }
         const float nz = e.noise ? e.noise[n * e.noise_nstride + p] * nstr : 0.f;
         const float yv = smc::epi_y(uv, dv, nz, bv, e.act, e.alpha, e.gain, e.clamp);
         const float dz = smc::act_grad_y(e.act, g[base + p], yv, e.alpha, e.gain, e.clamp);
@@ -632,6 +644,7 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const float* g, const floa
 
 // float4 form (hw % 4 == 0): each thread owns AB_V float4 groups of one plane, all loads issued first.
 constexpr int AB_V = 4;
+template <bool FROMY>
 __global__ __launch_bounds__(256) void act_bwd_vec4_kernel(const float* g, const float* u, float* du, float* dd, int c,
                                                            int64_t hw, Epi e) {
     __shared__ float red[4];
@@ -643,7 +656,7 @@ __global__ __launch_bounds__(256) void act_bwd_vec4_kernel(const float* g, const
     const int64_t hw4 = hw >> 2;
     const float4* g4 = reinterpret_cast<const float4*>(g + nc * hw);
     const float4* u4 = reinterpret_cast<const float4*>(u + nc * hw);
-    const float4* n4 = e.noise ? reinterpret_cast<const float4*>(e.noise + n * e.noise_nstride) : nullptr;
+    const float4* n4 = !FROMY && e.noise ? reinterpret_cast<const float4*>(e.noise + n * e.noise_nstride) : nullptr;
     float4* du4 = reinterpret_cast<float4*>(du + nc * hw);
     float part = 0.f;
     const int64_t q0 = (int64_t)blockIdx.x * 256 * AB_V + threadIdx.x;
@@ -666,6 +679,10 @@ __global__ __launch_bounds__(256) void act_bwd_vec4_kernel(const float* g, const
         float r[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+            if constexpr (FROMY) {
+                r[j] = smc::act_grad_y(e.act, ga[j], ua[j], e.alpha, e.gain, e.clamp) * dv;
+                continue;
+            }
             const float yv = smc::epi_y(ua[j], dv, na[j] * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
             const float dz = smc::act_grad_y(e.act, ga[j], yv, e.alpha, e.gain, e.clamp);
             r[j] = dz * dv;
@@ -828,20 +845,24 @@ SMC_API int smc_modconv_act_bwd_f32(const float* g, const float* u, float* du, f
                                     const smc_conv_epilogue* epi, void* stream) {
     SMC_CHECK(g && u && du && n >= 1 && c >= 1 && h >= 1 && w >= 1, "smc_modconv_act_bwd_f32: bad args");
     SMC_CHECK(epi && epi->mode == SMC_EPI_MODACT, "smc_modconv_act_bwd_f32: needs a MODACT epilogue");
+    const bool from_y = epi->grad_from_y != 0;
+    SMC_CHECK(!from_y || !dd, "smc_modconv_act_bwd_f32: dd needs u (grad_from_y set)");
     const int64_t hw = (int64_t)h * w;
     const int64_t planes = (int64_t)n * c;
-    const uintptr_t align = (uintptr_t)g | (uintptr_t)u | (uintptr_t)du | (uintptr_t)epi->noise;
-    if (hw % 4 == 0 && (!epi->noise || epi->noise_nstride % 4 == 0) && align % 16 == 0) {
-        SMC_CHECK(planes < 65536, "smc_modconv_act_bwd_f32: too many planes");
-        hipLaunchKernelGGL(act_bwd_vec4_kernel, dim3((unsigned)smc::ceil_div(hw / 4, 256 * AB_V), (unsigned)planes),
-                           dim3(256), 0, smc::as_stream(stream), g, u, du, dd, c, hw, to_epi(epi));
+    SMC_CHECK(planes < 65536, "smc_modconv_act_bwd_f32: too many planes");
+    const uintptr_t align = (uintptr_t)g | (uintptr_t)u | (uintptr_t)du | (uintptr_t)(from_y ? nullptr : epi->noise);
+    hipStream_t st = smc::as_stream(stream);
+    if (hw % 4 == 0 && (from_y || !epi->noise || epi->noise_nstride % 4 == 0) && align % 16 == 0) {
+        const dim3 grid((unsigned)smc::ceil_div(hw / 4, 256 * AB_V), (unsigned)planes);
+        if (from_y) hipLaunchKernelGGL(act_bwd_vec4_kernel<true>, grid, dim3(256), 0, st, g, u, du, dd, c, hw, to_epi(epi));
+        else hipLaunchKernelGGL(act_bwd_vec4_kernel<false>, grid, dim3(256), 0, st, g, u, du, dd, c, hw, to_epi(epi));
         return smc::check_launch("smc_modconv_act_bwd_f32");
     }
     int64_t per_plane = smc::ceil_div(hw, 256 * 8);  // ~8 elements per thread
     if (per_plane < 1) per_plane = 1;
-    SMC_CHECK(planes < 65536, "smc_modconv_act_bwd_f32: too many planes");
-    hipLaunchKernelGGL(act_bwd_kernel, dim3((unsigned)per_plane, (unsigned)planes), dim3(256), 0,
-                       smc::as_stream(stream), g, u, du, dd, c, hw, to_epi(epi));
+    const dim3 grid((unsigned)per_plane, (unsigned)planes);
+    if (from_y) hipLaunchKernelGGL(act_bwd_kernel<true>, grid, dim3(256), 0, st, g, u, du, dd, c, hw, to_epi(epi));
+    else hipLaunchKernelGGL(act_bwd_kernel<false>, grid, dim3(256), 0, st, g, u, du, dd, c, hw, to_epi(epi));
     return smc::check_launch("smc_modconv_act_bwd_f32");
 }
 
@@ -885,20 +906,26 @@ SMC_API int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* 
         smc::set_error("smc_modconv_blur_act_bwd_f32: only the 4x4 FIR has a fused kernel (got %dx%d)", fh, fw);
         return SMC_ERR_UNSUPPORTED;
     }
+    const bool from_y = epi->grad_from_y != 0;
+    SMC_CHECK(!from_y || !dd, "smc_modconv_blur_act_bwd_f32: dd needs u (grad_from_y set)");
     hipStream_t st = smc::as_stream(stream);
     dim3 grid((unsigned)smc::ceil_div(t_w, kFW), (unsigned)smc::ceil_div(t_h, kFH), (unsigned)(n * c));
-    const uintptr_t al = (uintptr_t)g | (uintptr_t)u | (uintptr_t)epi->noise;
-    if (u_w % 4 == 0 && epi->noise_nstride % 4 == 0 && (al & 15) == 0 && padx0 <= 4 && fw - 1 - padx0 <= 4) {
-        hipLaunchKernelGGL((blur_act_bwd_v4<4, 4>), grid, dim3(256), 0, st, g, u, dt, dd, c, u_h, u_w, t_h, t_w, tp_w, f,
-                           padx0, pady0, fgain, flip, to_epi(epi));
-        return smc::check_launch("smc_modconv_blur_act_bwd_f32");
+    const Epi e = to_epi(epi);
+    const uintptr_t al = (uintptr_t)g | (uintptr_t)u | (uintptr_t)(from_y ? nullptr : epi->noise);
+    const int64_t nstr = from_y ? 0 : epi->noise_nstride;
+#define SMC_BLUR_BWD(KERNEL)                                                                                       \
+    hipLaunchKernelGGL(KERNEL, grid, dim3(256), 0, st, g, u, dt, dd, c, u_h, u_w, t_h, t_w, tp_w, f, padx0, pady0, \
+                       fgain, flip, e)
+    if (u_w % 4 == 0 && nstr % 4 == 0 && (al & 15) == 0 && padx0 <= 4 && fw - 1 - padx0 <= 4) {
+        if (from_y) SMC_BLUR_BWD((blur_act_bwd_v4<4, 4, true>));
+        else SMC_BLUR_BWD((blur_act_bwd_v4<4, 4, false>));
+    } else if (u_w % 2 == 0 && padx0 % 2 == 0 && nstr % 2 == 0 && ((al & 7) == 0)) {
+        if (from_y) SMC_BLUR_BWD((blur_act_bwd_fast<4, 4, true, true>));
+        else SMC_BLUR_BWD((blur_act_bwd_fast<4, 4, true, false>));
+    } else {
+        if (from_y) SMC_BLUR_BWD((blur_act_bwd_fast<4, 4, false, true>));
+        else SMC_BLUR_BWD((blur_act_bwd_fast<4, 4, false, false>));
     }
-    const bool v2 = u_w % 2 == 0 && padx0 % 2 == 0 && epi->noise_nstride % 2 == 0 && ((al & 7) == 0);
-    if (v2)
-        hipLaunchKernelGGL((blur_act_bwd_fast<4, 4, true>), grid, dim3(256), 0, st, g, u, dt, dd, c, u_h, u_w, t_h, t_w,
-                           tp_w, f, padx0, pady0, fgain, flip, to_epi(epi));
-    else
-        hipLaunchKernelGGL((blur_act_bwd_fast<4, 4>), grid, dim3(256), 0, st, g, u, dt, dd, c, u_h, u_w, t_h, t_w, tp_w,
-                           f, padx0, pady0, fgain, flip, to_epi(epi));
+#undef SMC_BLUR_BWD
     return smc::check_launch("smc_modconv_blur_act_bwd_f32");
 }

@@ -162,8 +162,11 @@ class ModConvFn(torch.autograd.Function):
             _hip.call("smc_modconv_demod_f32", _hip.ptr(styles), _hip.ptr(P.wsq), _hip.ptr(d), n, cin, P.cout, 1e-8,
                       _hip.stream())
         save = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        # the activation mask of the backward needs only y; u is kept only where the style gradient needs
+        # dd = sum dz * u (the trainable layers): every other layer skips the u store (grad_from_y backward)
+        from_y = save and not ctx.needs_input_grad[1]
         y = torch.empty(n, P.cout, r_h, r_w, device=x.device, dtype=torch.float32)
-        u = torch.empty_like(y) if save else None
+        u = torch.empty_like(y) if save and not from_y else None
         nz, nstride = _noise_args(noise)
         epi = _epilogue(_hip.EPI_MODACT, d, nz, nstride, strength, spec.bias, spec.act, spec.alpha, gain, clamp, u)
         phases, nph, th, tw = P.fwd_phases(h, w)
@@ -182,7 +185,8 @@ class ModConvFn(torch.autograd.Function):
                       _hip.ptr(f), fh, fw, 1, 1, 4.0, 0, ctypes.byref(epi), _hip.stream())
         ctx.spec, ctx.gain, ctx.clamp = spec, gain, clamp
         ctx.noise, ctx.nstride, ctx.strength = nz, nstride, strength
-        ctx.save_for_backward(x, styles, d, u)
+        ctx.from_y = from_y
+        ctx.save_for_backward(x, styles, d, y if from_y else u)
         return y
 
     @staticmethod
@@ -198,6 +202,8 @@ class ModConvFn(torch.autograd.Function):
         dd = torch.zeros(n, P.cout, device=x.device, dtype=torch.float32) if (need_ds and spec.demodulate) else None
         epi = _epilogue(_hip.EPI_MODACT, d, ctx.noise, ctx.nstride, ctx.strength, spec.bias, spec.act, spec.alpha,
                         ctx.gain, ctx.clamp)
+        epi.grad_from_y = 1 if ctx.from_y else 0   # `u` below is then the saved forward output y
+        assert dd is None or not ctx.from_y
         if spec.up == 1:
             g = torch.empty_like(u)
             _hip.call("smc_modconv_act_bwd_f32", gy.data_ptr(), u.data_ptr(), g.data_ptr(), _hip.ptr(dd), n, P.cout,

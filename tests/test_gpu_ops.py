@@ -345,10 +345,57 @@ def test_blur_act_load_paths(n, c, h):
 
     dt0, dd0 = bwd(g, u0)
     dt1, dd1 = bwd(_misaligned(g), _misaligned(u0))
+
+    def bwd_from_y(gb, yb):   # grad_from_y: the saved forward output instead of u, no dd
+        dt = torch.full((n, c, th, th), float("nan"), device=DEV)
+        epi = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 1.0)
+        epi.grad_from_y = 1
+        _hip.call("smc_modconv_blur_act_bwd_f32", gb.data_ptr(), yb.data_ptr(), dt.data_ptr(), None, n, c,
+                  r, r, th, th, 0, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epi), st)
+        return dt
+
+    dt2 = bwd_from_y(g, y0)
+    dt3 = bwd_from_y(_misaligned(g), _misaligned(y0))
     torch.cuda.synchronize()
     assert torch.isfinite(dt0).all()
     assert torch.equal(dt0, dt1), "dT scalar vs 16-B loads"
     close(dd0, dd1, 1e-6, "dd")
+    # y = epi_y(u) bit for bit, so the mask and dT are identical
+    assert torch.equal(dt2, dt0), "dT from y vs from u"
+    assert torch.equal(dt3, dt0), "dT from y, scalar loads"
+
+
+@pytest.mark.parametrize("hw", [(64, 64), (7, 9)])
+def test_act_bwd_from_y(hw):
+    """conv1's epilogue backward (smc_modconv_act_bwd_f32) from the saved output y (grad_from_y: layers whose styles
+    need no gradient keep no u) equals the u path bit for bit (float4 and scalar kernels)."""
+    import ctypes
+    from stylemc_amd import _hip, modconv
+    gen = torch.Generator().manual_seed(22)
+    n, c = 2, 8
+    h, w = hw
+    u = torch.randn(n, c, h, w, generator=gen).to(DEV)
+    g = torch.randn(n, c, h, w, generator=gen).to(DEV)
+    d = (torch.rand(n, c, generator=gen) + 0.5).to(DEV)
+    noise = torch.randn(h, w, generator=gen).to(DEV)
+    strength = torch.tensor(0.3, device=DEV)
+    bias = (torch.randn(c, generator=gen) * 0.1).to(DEV)
+    st = _hip.stream()
+    y = torch.empty_like(u)
+    epi = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 1.0)
+    _hip.call("smc_modconv_epilogue_f32", u.data_ptr(), 1, 0, y.data_ptr(), n, c, h, w, ctypes.byref(epi), st)
+    du0, du1 = torch.empty_like(u), torch.empty_like(u)
+    dd = torch.zeros(n, c, device=DEV)
+    _hip.call("smc_modconv_act_bwd_f32", g.data_ptr(), u.data_ptr(), du0.data_ptr(), dd.data_ptr(), n, c, h, w,
+              ctypes.byref(epi), st)
+    epi.grad_from_y = 1
+    _hip.call("smc_modconv_act_bwd_f32", g.data_ptr(), y.data_ptr(), du1.data_ptr(), None, n, c, h, w,
+              ctypes.byref(epi), st)
+    torch.cuda.synchronize()
+    assert torch.equal(du0, du1)
+    with pytest.raises(RuntimeError):   # dd needs u
+        _hip.call("smc_modconv_act_bwd_f32", g.data_ptr(), y.data_ptr(), du1.data_ptr(), dd.data_ptr(), n, c, h, w,
+                  ctypes.byref(epi), st)
 
 
 def test_conv_gemm_2gib_input_fallback():

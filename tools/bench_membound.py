@@ -77,6 +77,14 @@ def main():
                       r, r, th, th, tp, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epib), st)
         us = timeit(blur_bp)
         print(f"r={r:5d} c={c:4d} blur_act_bwd_pitch{tp} {us:8.1f} us  {byt / us / 1e3:7.0f} GB/s")
+        epiy = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 256.0)
+        epiy.grad_from_y = 1
+
+        def blur_by():
+            _hip.call("smc_modconv_blur_act_bwd_f32", g.data_ptr(), y.data_ptr(), dtp.data_ptr(), None, n, c,
+                      r, r, th, th, tp, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epiy), st)
+        us = timeit(blur_by)
+        print(f"r={r:5d} c={c:4d} blur_act_bwd_from_y {us:8.1f} us  {byt / us / 1e3:7.0f} GB/s")
         du = torch.empty_like(y)
 
         def actb():
