@@ -179,6 +179,16 @@ int smc_torgb_fwd_f32(const float* x, const float* w, const float* s, const floa
 int smc_torgb_bwd_f32(const float* g, const float* y, const float* w, const float* s, float* dx, int n, int cin,
                       int cout, int h, int w_, float clamp, int scale, int accumulate, void* stream);
 
+/* Block-tail backward (the synthesis block output y = conv1's output feeds this block's ToRGB and the next block's
+ * conv0): du[n,k,p] = act'(g_next[n,k,p] + (ToRGB^T g_rgb)[n,k,p]; y[n,k,p]) * d[n,k] with conv1's MODACT epilogue
+ * `epi` (grad_from_y must be set: y is conv1's output; its d/act/alpha/gain/clamp), ToRGB^T as smc_torgb_bwd_f32
+ * with scale = 1 (g_rgb masked by |y_rgb| < clamp_rgb), g_next may be NULL (the last block).  Bit-identical to
+ * smc_torgb_bwd_f32 + the sum + smc_modconv_act_bwd_f32 (grad_from_y).  Replaces the autograd sum of the two
+ * gradients of [upstream] SynthesisBlock's `x` (utils.py:47 torgb + the next block's conv0). */
+int smc_torgb_act_bwd_f32(const float* g_rgb, const float* y_rgb, const float* w, const float* s, float clamp_rgb,
+                          const float* g_next, const float* y, float* du, int n, int cin, int cout, int h, int w_,
+                          const smc_conv_epilogue* epi, void* stream);
+
 /* IDLoss face crop (id_loss.py:20-23): y[p] = adaptive_avg_pool(crop(adaptive_avg_pool(x[p], (pool_h, pool_w)),
  * [crop_y0 : crop_y0+crop_h, crop_x0 : crop_x0+crop_w]), (out_h, out_w)) for `planes` planes; the first pool
  * must be an integer factor (in = pool * k, else SMC_ERR_UNSUPPORTED).  The backward writes the whole input

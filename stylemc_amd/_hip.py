@@ -67,6 +67,7 @@ _SIGS = {
     "smc_modconv_demod_bwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, P]),
     "smc_torgb_fwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, P]),
     "smc_torgb_bwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_int, P]),
+    "smc_torgb_act_bwd_f32": (c_int, [P, P, P, P, c_float, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "smc_face_crop_f32": (c_int, [P, c_int64] + [c_int] * 10 + [P, P]),
     "smc_face_crop_bwd_f32": (c_int, [P, c_int64] + [c_int] * 10 + [P, P]),
     "smc_clip_unprocess_f32": (c_int, [P] + [c_int] * 6 + [P, P, P, P]),

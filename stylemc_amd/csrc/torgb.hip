@@ -138,6 +138,72 @@ __global__ __launch_bounds__(256) void torgb_bwd_kernel(const float* g, const fl
     }
 }
 
+// Block-tail backward: a synthesis block's output y (conv1's output, read by this block's ToRGB and by the next
+// block's conv0) gets g_y = g_next + ToRGB^T(g_rgb), and conv1's epilogue backward turns it into du = act'(g_y; y) *
+// d[n,k] -- three passes (ToRGB data gradient, autograd's sum, act_bwd) in one.  The ToRGB gradient and the sum are
+// the same fp32 operations as the separate kernels (a + b is commutative), and the epilogue backward is act_bwd's
+// grad_from_y form, so du is bit-identical to the unfused path.
+template <bool VEC>
+__global__ __launch_bounds__(256) void torgb_act_bwd_kernel(const float* g_rgb, const float* y_rgb, const float* w,
+                                                            const float* s, float clamp_rgb, const float* g_next,
+                                                            const float* y, float* du, int cin, int cout, int64_t hw,
+                                                            const float* d, int act, float alpha, float gain,
+                                                            float clamp) {
+    __shared__ float ws[kMaxOut * kMaxIn];
+    const int nn = blockIdx.y;
+    for (int i = threadIdx.x; i < cout * cin; i += 256) {
+        const int c = i / cin, k = i - c * cin;
+        ws[i] = w[i] * s[(int64_t)nn * cin + k];
+    }
+    __syncthreads();
+    constexpr int V = VEC ? 4 : 1;
+    const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
+    if (p0 >= hw) return;
+    float gm[kMaxOut][V];
+#pragma unroll
+    for (int c = 0; c < kMaxOut; ++c) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) gm[c][v] = 0.f;
+        if (c >= cout) continue;
+        const int64_t off = ((int64_t)nn * cout + c) * hw + p0;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const float yv = y_rgb[off + v];
+            const bool pass = clamp_rgb < 0.f || (yv > -clamp_rgb && yv < clamp_rgb);
+            gm[c][v] = pass ? g_rgb[off + v] : 0.f;
+        }
+    }
+    const int64_t base = (int64_t)nn * cin * hw + p0;
+    for (int k = 0; k < cin; ++k) {
+        const int64_t off = base + (int64_t)k * hw;
+        float gn[V], yk[V], r[V];
+        if (VEC) {
+            const float4 a = g_next ? *reinterpret_cast<const float4*>(g_next + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 b = *reinterpret_cast<const float4*>(y + off);
+            gn[0] = a.x; gn[V > 1 ? 1 : 0] = a.y; gn[V > 2 ? 2 : 0] = a.z; gn[V > 3 ? 3 : 0] = a.w;
+            yk[0] = b.x; yk[V > 1 ? 1 : 0] = b.y; yk[V > 2 ? 2 : 0] = b.z; yk[V > 3 ? 3 : 0] = b.w;
+        } else {
+            gn[0] = g_next ? g_next[off] : 0.f;
+            yk[0] = y[off];
+        }
+        const float dk = d ? d[(int64_t)nn * cin + k] : 1.f;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            float t = 0.f;
+#pragma unroll
+            for (int c = 0; c < kMaxOut; ++c) {
+                if (c >= cout) break;
+                t += ws[c * cin + k] * gm[c][v];
+            }
+            const float gy = g_next ? gn[v] + t : t;
+            r[v] = smc::act_grad_y(act, gy, yk[v], alpha, gain, clamp) * dk;
+        }
+        if (VEC) *reinterpret_cast<float4*>(du + off) = make_float4(r[0], r[V > 1 ? 1 : 0], r[V > 2 ? 2 : 0],
+                                                                    r[V > 3 ? 3 : 0]);
+        else du[off] = r[0];
+    }
+}
+
 // Low-resolution forms (hw <= kSmallHw: the 4..64-px blocks, 512 input channels).  The per-position kernels
 // above give each thread the whole channel reduction, which at these sizes is 1-4 workgroups per image and a
 // chain of 64 dependent load rounds (~90 us for 16 positions).  Here the channels are split over the
@@ -280,4 +346,30 @@ SMC_API int smc_torgb_bwd_f32(const float* g, const float* y, const float* w, co
     else hipLaunchKernelGGL(torgb_bwd_kernel<false>, grid, dim3(256), 0, smc::as_stream(stream), g, y, w, s, dx, cin,
                             cout, hw, clamp, scale, accumulate);
     return smc::check_launch("smc_torgb_bwd_f32");
+}
+
+SMC_API int smc_torgb_act_bwd_f32(const float* g_rgb, const float* y_rgb, const float* w, const float* s,
+                                  float clamp_rgb, const float* g_next, const float* y, float* du, int n, int cin,
+                                  int cout, int h, int w_, const smc_conv_epilogue* epi, void* stream) {
+    SMC_CHECK(g_rgb && y_rgb && w && s && y && du && n >= 1 && cin >= 1 && h >= 1 && w_ >= 1,
+              "smc_torgb_act_bwd_f32: bad args");
+    SMC_CHECK(epi && epi->mode == SMC_EPI_MODACT && epi->grad_from_y,
+              "smc_torgb_act_bwd_f32: needs conv1's MODACT epilogue with grad_from_y");
+    SMC_CHECK(n < 65536, "smc_torgb_act_bwd_f32: batch too large");
+    if (cout < 1 || cout > kMaxOut || cin > kMaxIn) {
+        smc::set_error("smc_torgb_act_bwd_f32: cout=%d (max %d) cin=%d (max %d)", cout, kMaxOut, cin, kMaxIn);
+        return SMC_ERR_UNSUPPORTED;
+    }
+    const int64_t hw = (int64_t)h * w_;
+    const uintptr_t al = (uintptr_t)g_next | (uintptr_t)y | (uintptr_t)du;
+    const bool vec = hw % 4 == 0 && (al & 15) == 0;
+    const int64_t per = vec ? hw / 4 : hw;
+    dim3 grid((unsigned)smc::ceil_div(per, 256), (unsigned)n);
+    if (vec)
+        hipLaunchKernelGGL(torgb_act_bwd_kernel<true>, grid, dim3(256), 0, smc::as_stream(stream), g_rgb, y_rgb, w, s,
+                           clamp_rgb, g_next, y, du, cin, cout, hw, epi->d, epi->act, epi->alpha, epi->gain, epi->clamp);
+    else
+        hipLaunchKernelGGL(torgb_act_bwd_kernel<false>, grid, dim3(256), 0, smc::as_stream(stream), g_rgb, y_rgb, w, s,
+                           clamp_rgb, g_next, y, du, cin, cout, hw, epi->d, epi->act, epi->alpha, epi->gain, epi->clamp);
+    return smc::check_launch("smc_torgb_act_bwd_f32");
 }

@@ -145,65 +145,69 @@ def _noise_args(noise):
     return noise, noise.shape[2] * noise.shape[3]
 
 
-class ModConvFn(torch.autograd.Function):
-    """y = modconv_epilogue(conv(x * s, W)); grads w.r.t. x and s only."""
+def _modconv_fwd(ctx, x, styles, spec, noise, strength, gain, clamp, need_dx, need_ds):
+    """The modconv forward (GEMM + fused epilogue); sets ctx's backward state, returns y and the tensors the
+    backward needs (x, styles, d, and u -- or y itself where the styles need no gradient)."""
+    x = x.contiguous()
+    styles = styles.contiguous()
+    P = spec.packed
+    n, cin, h, w = x.shape
+    assert cin == P.cin and styles.shape == (n, cin), (x.shape, styles.shape, P.cin)
+    r_h, r_w = h * spec.up, w * spec.up
+    d = None
+    if spec.demodulate:
+        d = torch.empty(n, P.cout, device=x.device, dtype=torch.float32)
+        _hip.call("smc_modconv_demod_f32", _hip.ptr(styles), _hip.ptr(P.wsq), _hip.ptr(d), n, cin, P.cout, 1e-8,
+                  _hip.stream())
+    save = need_dx or need_ds
+    # the activation mask of the backward needs only y; u is kept only where the style gradient needs
+    # dd = sum dz * u (the trainable layers): every other layer skips the u store (grad_from_y backward)
+    from_y = save and not need_ds
+    y = torch.empty(n, P.cout, r_h, r_w, device=x.device, dtype=torch.float32)
+    u = torch.empty_like(y) if save and not from_y else None
+    nz, nstride = _noise_args(noise)
+    epi = _epilogue(_hip.EPI_MODACT, d, nz, nstride, strength, spec.bias, spec.act, spec.alpha, gain, clamp, u)
+    phases, nph, th, tw = P.fwd_phases(h, w)
+    wbytes = 4 * P.k * P.k * cin * P.cout
+    if spec.up == 1:
+        gemm(x, y, phases, nph, cin, P.cout, s=styles, epi=epi,
+             alg_flops=conv_flops(n, cin, P.cout, r_h, r_w, P.k * P.k),
+             alg_bytes=4 * x.numel() + 4 * y.numel() * (2 if u is not None else 1) + wbytes)
+    else:
+        t = torch.empty(n, P.cout, th, tw, device=x.device, dtype=torch.float32)
+        gemm(x, t, phases, nph, cin, P.cout, s=styles, epi=_epilogue(_hip.EPI_STORE),
+             alg_flops=conv_flops(n, cin, P.cout, h, w, 9), alg_bytes=4 * x.numel() + 4 * t.numel() + wbytes)
+        f = spec.filter.to(x.device)
+        fh, fw = f.shape
+        _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, P.cout, th, tw, 0, r_h, r_w,
+                  _hip.ptr(f), fh, fw, 1, 1, 4.0, 0, ctypes.byref(epi), _hip.stream())
+    ctx.spec, ctx.gain, ctx.clamp = spec, gain, clamp
+    ctx.noise, ctx.nstride, ctx.strength = nz, nstride, strength
+    ctx.from_y = from_y
+    return y, (x, styles, d, y if from_y else u)
 
-    @staticmethod
-    def forward(ctx, x, styles, spec, noise, strength, gain, clamp):
-        x = x.contiguous()
-        styles = styles.contiguous()
-        P = spec.packed
-        n, cin, h, w = x.shape
-        assert cin == P.cin and styles.shape == (n, cin), (x.shape, styles.shape, P.cin)
-        r_h, r_w = h * spec.up, w * spec.up
-        d = None
-        if spec.demodulate:
-            d = torch.empty(n, P.cout, device=x.device, dtype=torch.float32)
-            _hip.call("smc_modconv_demod_f32", _hip.ptr(styles), _hip.ptr(P.wsq), _hip.ptr(d), n, cin, P.cout, 1e-8,
-                      _hip.stream())
-        save = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
-        # the activation mask of the backward needs only y; u is kept only where the style gradient needs
-        # dd = sum dz * u (the trainable layers): every other layer skips the u store (grad_from_y backward)
-        from_y = save and not ctx.needs_input_grad[1]
-        y = torch.empty(n, P.cout, r_h, r_w, device=x.device, dtype=torch.float32)
-        u = torch.empty_like(y) if save and not from_y else None
-        nz, nstride = _noise_args(noise)
-        epi = _epilogue(_hip.EPI_MODACT, d, nz, nstride, strength, spec.bias, spec.act, spec.alpha, gain, clamp, u)
-        phases, nph, th, tw = P.fwd_phases(h, w)
-        wbytes = 4 * P.k * P.k * cin * P.cout
-        if spec.up == 1:
-            gemm(x, y, phases, nph, cin, P.cout, s=styles, epi=epi,
-                 alg_flops=conv_flops(n, cin, P.cout, r_h, r_w, P.k * P.k),
-                 alg_bytes=4 * x.numel() + 4 * y.numel() * (2 if save else 1) + wbytes)
-        else:
-            t = torch.empty(n, P.cout, th, tw, device=x.device, dtype=torch.float32)
-            gemm(x, t, phases, nph, cin, P.cout, s=styles, epi=_epilogue(_hip.EPI_STORE),
-                 alg_flops=conv_flops(n, cin, P.cout, h, w, 9), alg_bytes=4 * x.numel() + 4 * t.numel() + wbytes)
-            f = spec.filter.to(x.device)
-            fh, fw = f.shape
-            _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, P.cout, th, tw, 0, r_h, r_w,
-                      _hip.ptr(f), fh, fw, 1, 1, 4.0, 0, ctypes.byref(epi), _hip.stream())
-        ctx.spec, ctx.gain, ctx.clamp = spec, gain, clamp
-        ctx.noise, ctx.nstride, ctx.strength = nz, nstride, strength
-        ctx.from_y = from_y
-        ctx.save_for_backward(x, styles, d, y if from_y else u)
-        return y
 
-    @staticmethod
-    def backward(ctx, gy):
-        x, styles, d, u = ctx.saved_tensors
-        spec = ctx.spec
-        P = spec.packed
-        n, cin, h, w = x.shape
-        need_dx, need_ds = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        if not (need_dx or need_ds):
-            return None, None, None, None, None, None, None
+def _modconv_epi_bwd(ctx, d):
+    """conv's MODACT epilogue as its backward kernels see it (grad_from_y: their `u` is the saved y)."""
+    spec = ctx.spec
+    epi = _epilogue(_hip.EPI_MODACT, d, ctx.noise, ctx.nstride, ctx.strength, spec.bias, spec.act, spec.alpha,
+                    ctx.gain, ctx.clamp)
+    epi.grad_from_y = 1 if ctx.from_y else 0
+    return epi
+
+
+def _modconv_bwd(ctx, saved, gy, need_dx, need_ds, g=None):
+    """The modconv backward from the output gradient gy -- or from g, the epilogue's backward already applied
+    (du = act'(gy; y) * d, a 1:1 layer whose styles need no gradient).  Returns (dx, ds)."""
+    x, styles, d, u = saved
+    spec = ctx.spec
+    P = spec.packed
+    n, cin, h, w = x.shape
+    dd = torch.zeros(n, P.cout, device=x.device, dtype=torch.float32) if (need_ds and spec.demodulate) else None
+    assert dd is None or not ctx.from_y
+    if g is None:
         gy = gy.contiguous()
-        dd = torch.zeros(n, P.cout, device=x.device, dtype=torch.float32) if (need_ds and spec.demodulate) else None
-        epi = _epilogue(_hip.EPI_MODACT, d, ctx.noise, ctx.nstride, ctx.strength, spec.bias, spec.act, spec.alpha,
-                        ctx.gain, ctx.clamp)
-        epi.grad_from_y = 1 if ctx.from_y else 0   # `u` below is then the saved forward output y
-        assert dd is None or not ctx.from_y
+        epi = _modconv_epi_bwd(ctx, d)
         if spec.up == 1:
             g = torch.empty_like(u)
             _hip.call("smc_modconv_act_bwd_f32", gy.data_ptr(), u.data_ptr(), g.data_ptr(), _hip.ptr(dd), n, P.cout,
@@ -220,27 +224,114 @@ class ModConvFn(torch.autograd.Function):
             _hip.call("smc_modconv_blur_act_bwd_f32", gy.data_ptr(), u.data_ptr(), g.data_ptr(), _hip.ptr(dd), n,
                       P.cout, u.shape[2], u.shape[3], th, tw, pitch, _hip.ptr(f), fh, fw, fw - 2, fh - 2, 4.0, 1,
                       ctypes.byref(epi), _hip.stream())
-        dx = torch.empty_like(x) if need_dx else None
-        dxs = torch.empty_like(x) if need_ds else None
-        if need_dx:
-            ebw = _epilogue(_hip.EPI_MODACT, d=styles, act="linear", u_save=dxs)
-            out = dx
-        else:
-            ebw = _epilogue(_hip.EPI_STORE)
-            out = dxs
-        phases, nph = P.bwd_phases(h, w)
-        g_bytes = 4 * g.numel() if spec.up == 1 else 4 * n * P.cout * (2 * h + 1) * (2 * w + 1)
-        gemm(g, out, phases, nph, P.cout, cin, epi=ebw, alg_flops=conv_flops(n, P.cout, cin, h, w, P.k * P.k),
-             alg_bytes=g_bytes + 4 * out.numel() * (2 if (need_dx and need_ds) else 1) + 4 * P.k * P.k * cin * P.cout)
-        ds = None
-        if need_ds:
-            ds = torch.empty(n, cin, device=x.device, dtype=torch.float32)
-            _hip.call("smc_channel_dot_f32", dxs.data_ptr(), x.data_ptr(), None, ds.data_ptr(), None, n * cin, h * w, 0,
-                      _hip.stream())
-            if spec.demodulate:
-                _hip.call("smc_modconv_demod_bwd_f32", styles.data_ptr(), d.data_ptr(), dd.data_ptr(),
-                          P.wsq.data_ptr(), ds.data_ptr(), n, cin, P.cout, _hip.stream())
+    else:
+        assert spec.up == 1 and dd is None
+    dx = torch.empty_like(x) if need_dx else None
+    dxs = torch.empty_like(x) if need_ds else None
+    if need_dx:
+        ebw = _epilogue(_hip.EPI_MODACT, d=styles, act="linear", u_save=dxs)
+        out = dx
+    else:
+        ebw = _epilogue(_hip.EPI_STORE)
+        out = dxs
+    phases, nph = P.bwd_phases(h, w)
+    g_bytes = 4 * g.numel() if spec.up == 1 else 4 * n * P.cout * (2 * h + 1) * (2 * w + 1)
+    gemm(g, out, phases, nph, P.cout, cin, epi=ebw, alg_flops=conv_flops(n, P.cout, cin, h, w, P.k * P.k),
+         alg_bytes=g_bytes + 4 * out.numel() * (2 if (need_dx and need_ds) else 1) + 4 * P.k * P.k * cin * P.cout)
+    ds = None
+    if need_ds:
+        ds = torch.empty(n, cin, device=x.device, dtype=torch.float32)
+        _hip.call("smc_channel_dot_f32", dxs.data_ptr(), x.data_ptr(), None, ds.data_ptr(), None, n * cin, h * w, 0,
+                  _hip.stream())
+        if spec.demodulate:
+            _hip.call("smc_modconv_demod_bwd_f32", styles.data_ptr(), d.data_ptr(), dd.data_ptr(),
+                      P.wsq.data_ptr(), ds.data_ptr(), n, cin, P.cout, _hip.stream())
+    return dx, ds
+
+
+class ModConvFn(torch.autograd.Function):
+    """y = modconv_epilogue(conv(x * s, W)); grads w.r.t. x and s only."""
+
+    @staticmethod
+    def forward(ctx, x, styles, spec, noise, strength, gain, clamp):
+        y, saved = _modconv_fwd(ctx, x, styles, spec, noise, strength, gain, clamp, ctx.needs_input_grad[0],
+                                ctx.needs_input_grad[1])
+        ctx.save_for_backward(*saved)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        need_dx, need_ds = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if not (need_dx or need_ds):
+            return None, None, None, None, None, None, None
+        dx, ds = _modconv_bwd(ctx, ctx.saved_tensors, gy, need_dx, need_ds)
         return dx, ds, None, None, None, None, None
+
+
+def _torgb_fwd(x, styles, w2d, bias, clamp):
+    n, cin, h, w = x.shape
+    cout = w2d.shape[0]
+    y = torch.empty(n, cout, h, w, device=x.device, dtype=torch.float32)
+    _hip.call("smc_torgb_fwd_f32", x.data_ptr(), _hip.ptr(w2d), styles.data_ptr(), _hip.ptr(bias), y.data_ptr(), n,
+              cin, cout, h, w, clamp, _hip.stream())
+    return y
+
+
+def _torgb_style_grad(gy, y, x, styles, w2d, clamp):
+    n, cin, h, w = x.shape
+    dxs = torch.empty_like(x)
+    _hip.call("smc_torgb_bwd_f32", gy.data_ptr(), y.data_ptr(), w2d.data_ptr(), styles.data_ptr(), dxs.data_ptr(), n,
+              cin, w2d.shape[0], h, w, clamp, 0, 0, _hip.stream())
+    ds = torch.empty(n, cin, device=x.device, dtype=torch.float32)
+    _hip.call("smc_channel_dot_f32", dxs.data_ptr(), x.data_ptr(), None, ds.data_ptr(), None, n * cin, h * w, 0,
+              _hip.stream())
+    return ds
+
+
+class ModConvToRGBFn(torch.autograd.Function):
+    """A synthesis block's conv1 (3x3 modconv) and the ToRGB layer reading its output y, as one Function:
+    returns (y, rgb).  y also feeds the next block's conv0, so its gradient is g_next + ToRGB^T(g_rgb); where
+    conv1's styles need no gradient the backward forms it and conv1's epilogue backward in one pass
+    (smc_torgb_act_bwd_f32) instead of a ToRGB data-gradient kernel, autograd's sum and the act backward
+    (utils.py:47 + [upstream] SynthesisBlock.forward; same numbers bit for bit)."""
+
+    @staticmethod
+    def forward(ctx, x, styles, spec, noise, strength, gain, clamp, s_rgb, w_rgb, b_rgb, clamp_rgb):
+        ctx.set_materialize_grads(False)
+        y, saved = _modconv_fwd(ctx, x, styles, spec, noise, strength, gain, clamp, ctx.needs_input_grad[0],
+                                ctx.needs_input_grad[1])
+        s_rgb = s_rgb.contiguous()
+        rgb = _torgb_fwd(y, s_rgb, w_rgb, b_rgb, clamp_rgb)
+        ctx.clamp_rgb = clamp_rgb
+        ctx.save_for_backward(*saved, y, s_rgb, w_rgb, rgb)
+        return y, rgb
+
+    @staticmethod
+    def backward(ctx, gy, grgb):
+        x, styles, d, u, y, s_rgb, w_rgb, rgb = ctx.saved_tensors
+        need_dx, need_ds, need_ds_rgb = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[7]
+        ds_rgb = None
+        if need_ds_rgb and grgb is not None:
+            ds_rgb = _torgb_style_grad(grgb.contiguous(), rgb, y, s_rgb, w_rgb, ctx.clamp_rgb)
+        dx = ds = None
+        if (need_dx or need_ds) and (gy is not None or grgb is not None):
+            saved = (x, styles, d, u)
+            n, c, h, w = y.shape
+            if grgb is not None and ctx.from_y and ctx.spec.up == 1:
+                g = torch.empty_like(y)
+                _hip.call("smc_torgb_act_bwd_f32", grgb.contiguous().data_ptr(), rgb.data_ptr(), w_rgb.data_ptr(),
+                          s_rgb.data_ptr(), ctx.clamp_rgb, _hip.ptr(gy.contiguous() if gy is not None else None),
+                          y.data_ptr(), g.data_ptr(), n, c, w_rgb.shape[0], h, w,
+                          ctypes.byref(_modconv_epi_bwd(ctx, d)), _hip.stream())
+                dx, ds = _modconv_bwd(ctx, saved, None, need_dx, need_ds, g=g)
+            else:
+                gtot = gy.contiguous().clone() if gy is not None else torch.zeros_like(y)
+                if grgb is not None:
+                    _hip.call("smc_torgb_bwd_f32", grgb.contiguous().data_ptr(), rgb.data_ptr(), w_rgb.data_ptr(),
+                              s_rgb.data_ptr(), gtot.data_ptr(), n, c, w_rgb.shape[0], h, w, ctx.clamp_rgb, 1, 1,
+                              _hip.stream())
+                dx, ds = _modconv_bwd(ctx, saved, gtot, need_dx, need_ds)
+        return dx, ds, None, None, None, None, None, ds_rgb, None, None, None
 
 
 class ToRGBFn(torch.autograd.Function):
@@ -250,11 +341,7 @@ class ToRGBFn(torch.autograd.Function):
     def forward(ctx, x, styles, weight2d, bias, clamp):
         x = x.contiguous()
         styles = styles.contiguous()
-        n, cin, h, w = x.shape
-        cout = weight2d.shape[0]
-        y = torch.empty(n, cout, h, w, device=x.device, dtype=torch.float32)
-        _hip.call("smc_torgb_fwd_f32", x.data_ptr(), _hip.ptr(weight2d), styles.data_ptr(), _hip.ptr(bias),
-                  y.data_ptr(), n, cin, cout, h, w, clamp, _hip.stream())
+        y = _torgb_fwd(x, styles, weight2d, bias, clamp)
         ctx.clamp = clamp
         ctx.save_for_backward(x, styles, weight2d, y)
         return y
@@ -263,20 +350,14 @@ class ToRGBFn(torch.autograd.Function):
     def backward(ctx, gy):
         x, styles, w2, y = ctx.saved_tensors
         n, cin, h, w = x.shape
-        cout = w2.shape[0]
         gy = gy.contiguous()
         dx = ds = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             _hip.call("smc_torgb_bwd_f32", gy.data_ptr(), y.data_ptr(), w2.data_ptr(), styles.data_ptr(),
-                      dx.data_ptr(), n, cin, cout, h, w, ctx.clamp, 1, 0, _hip.stream())
+                      dx.data_ptr(), n, cin, w2.shape[0], h, w, ctx.clamp, 1, 0, _hip.stream())
         if ctx.needs_input_grad[1]:
-            dxs = torch.empty_like(x)
-            _hip.call("smc_torgb_bwd_f32", gy.data_ptr(), y.data_ptr(), w2.data_ptr(), styles.data_ptr(),
-                      dxs.data_ptr(), n, cin, cout, h, w, ctx.clamp, 0, 0, _hip.stream())
-            ds = torch.empty(n, cin, device=x.device, dtype=torch.float32)
-            _hip.call("smc_channel_dot_f32", dxs.data_ptr(), x.data_ptr(), None, ds.data_ptr(), None, n * cin, h * w, 0,
-                      _hip.stream())
+            ds = _torgb_style_grad(gy, y, x, styles, w2, ctx.clamp)
         return dx, ds, None, None, None
 
 

@@ -93,7 +93,8 @@ class SynthesisLayer(torch.nn.Module):
                               lambda: modconv.LayerSpec(self.weight, self.bias, self.up, self.resample_filter,
                                                         demodulate=True, act=self.activation, alpha=alpha))
 
-    def forward(self, x, w, noise_mode="random", fused_modconv=True, gain=1):
+    def fn_args(self, x, w, noise_mode="random", gain=1):
+        """The ModConvFn argument tuple of forward(x, w, noise_mode, gain=gain)."""
         assert noise_mode in ("random", "const", "none")
         in_res = self.resolution // self.up
         assert x.shape[1:] == (self.weight.shape[1], in_res, in_res), (tuple(x.shape), self.weight.shape)
@@ -107,7 +108,10 @@ class SynthesisLayer(torch.nn.Module):
             strength = self.noise_strength.detach()
         act_gain = float(self.act_gain * gain)
         act_clamp = float(self.conv_clamp * gain) if self.conv_clamp is not None else -1.0
-        return modconv.ModConvFn.apply(x.float(), styles.float(), self.spec(), noise, strength, act_gain, act_clamp)
+        return x.float(), styles.float(), self.spec(), noise, strength, act_gain, act_clamp
+
+    def forward(self, x, w, noise_mode="random", fused_modconv=True, gain=1):
+        return modconv.ModConvFn.apply(*self.fn_args(x, w, noise_mode, gain))
 
 
 class ToRGBLayer(torch.nn.Module):
@@ -121,11 +125,15 @@ class ToRGBLayer(torch.nn.Module):
         self.weight_gain = 1 / math.sqrt(in_channels * kernel_size * kernel_size)
         self._w2d = _SpecCache()
 
-    def forward(self, x, w, fused_modconv=True):
+    def fn_args(self, x, w):
+        """The ToRGBFn argument tuple of forward(x, w)."""
         styles = self.affine(w) * self.weight_gain
         w2d = self._w2d.get(_version_key(self.weight), lambda: self.weight.detach()[:, :, 0, 0].float().contiguous())
         clamp = float(self.conv_clamp) if self.conv_clamp is not None else -1.0
-        return modconv.ToRGBFn.apply(x.float(), styles.float(), w2d, self.bias.detach().float().contiguous(), clamp)
+        return x.float(), styles.float(), w2d, self.bias.detach().float().contiguous(), clamp
+
+    def forward(self, x, w, fused_modconv=True):
+        return modconv.ToRGBFn.apply(*self.fn_args(x, w))
 
 
 class SynthesisBlock(torch.nn.Module):
@@ -157,6 +165,11 @@ class SynthesisBlock(torch.nn.Module):
         self.num_conv += 1
         self.torgb = ToRGBLayer(out_channels, img_channels, w_dim, conv_clamp=conv_clamp)
         self.num_torgb += 1
+
+    def conv1_torgb(self, x, w1, w_rgb, noise_mode="random"):
+        """conv1(x, w1) and the ToRGB of its output as one autograd Function (modconv.ModConvToRGBFn, whose
+        backward fuses the two gradients of the block output): returns (x, rgb) = (conv1 output, ToRGB output)."""
+        return modconv.ModConvToRGBFn.apply(*self.conv1.fn_args(x, w1, noise_mode), *self.torgb.fn_args(x, w_rgb)[1:])
 
     def forward(self, x, img, ws, force_fp32=False, fused_modconv=None, **layer_kwargs):
         rows = iter(ws.unbind(dim=1))

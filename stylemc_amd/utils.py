@@ -87,13 +87,15 @@ def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", del
         shapes = temp_shapes[k]
         if block.in_channels == 0:
             x = block.const.to(torch.float32).unsqueeze(0).repeat([styles.shape[0], 1, 1, 1])
-            x = block.conv1(x, rows[0][..., :shapes[0]], noise_mode=noise_mode)
+            w1 = rows[0][..., :shapes[0]]
         else:
             x = block.conv0(x, rows[0][..., :shapes[0]], noise_mode=noise_mode)
-            x = block.conv1(x, rows[1][..., :shapes[1]], noise_mode=noise_mode)
+            w1 = rows[1][..., :shapes[1]]
         if img is not None:
             img = upfirdn2d.upsample2d(img, block.resample_filter)
-        y = block.torgb(x, rows[-1][..., :shapes[2]])
+        # conv1 + ToRGB as one Function: the backward sums the block output's two gradients (ToRGB and the next
+        # block's conv0) inside conv1's epilogue backward
+        x, y = block.conv1_torgb(x, w1, rows[-1][..., :shapes[2]], noise_mode=noise_mode)
         img = img.add_(y) if img is not None else y
         row += width
     return img

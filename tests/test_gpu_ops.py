@@ -495,3 +495,47 @@ def test_synthesis_1024_vs_oracle():
     close(ds_p[:, T], ds_o[:, T], 2e-3, "dstyles trainable rows")
     cos = torch.nn.functional.cosine_similarity(ds_p.cpu().double().flatten(), ds_o.double().flatten(), dim=0)
     assert cos > 0.9999, cos
+
+
+@pytest.mark.parametrize("res,ch,styles_grad", [(128, 64, False), (64, 128, True), (1024, 32, False)])
+def test_conv1_torgb_fused_backward(res, ch, styles_grad):
+    """SynthesisBlock.conv1_torgb (modconv.ModConvToRGBFn: the block output's two gradients -- this block's ToRGB
+    and the next block's conv0 -- summed inside conv1's epilogue backward, smc_torgb_act_bwd_f32) against the
+    separate conv1 + ToRGB Functions with autograd's sum: bit-identical where conv1's styles need no gradient
+    (the fused kernel), 1e-6 otherwise (the same kernels in another order)."""
+    from stylemc_amd import networks
+    torch.manual_seed(5)
+    blk = networks.SynthesisBlock(ch, ch, 512, res, 3, is_last=False, conv_clamp=256).to(DEV)
+    with torch.no_grad():
+        for p_ in blk.parameters():
+            p_.copy_(torch.randn_like(p_) * (0.3 if p_.ndim <= 1 else 1.0))
+    n = 2
+    x0 = torch.randn(n, ch, res, res, device=DEV)
+    w1 = torch.randn(n, 512, device=DEV)
+    wr = torch.randn(n, 512, device=DEV)
+    g_next = torch.randn(n, ch, res, res, device=DEV)
+    g_rgb = torch.randn(n, 3, res, res, device=DEV)
+    outs = []
+    for fused in (True, False):
+        x = x0.clone().requires_grad_(True)
+        w = w1.clone().requires_grad_(styles_grad)
+        if fused:
+            y, rgb = blk.conv1_torgb(x, w, wr, noise_mode="const")
+        else:
+            y = blk.conv1(x, w, noise_mode="const")
+            rgb = blk.torgb(y, wr)
+        loss = (y * g_next).sum() + (rgb * g_rgb).sum()
+        grads = torch.autograd.grad(loss, [x, w] if styles_grad else [x])
+        outs.append((y.detach(), rgb.detach()) + tuple(grads))
+    for a, b, what in zip(outs[0], outs[1], ("y", "rgb", "dx", "dw")):
+        if styles_grad and what in ("dx", "dw"):
+            close(a, b, 1e-6, what)
+        else:
+            assert torch.equal(a, b), what
+    # the last block: ToRGB is the only consumer of y (no g_next)
+    x = x0.clone().requires_grad_(True)
+    y, rgb = blk.conv1_torgb(x, w1, wr, noise_mode="const")
+    (dxa,) = torch.autograd.grad((rgb * g_rgb).sum(), [x])
+    x = x0.clone().requires_grad_(True)
+    (dxb,) = torch.autograd.grad((blk.torgb(blk.conv1(x, w1, noise_mode="const"), wr) * g_rgb).sum(), [x])
+    assert torch.equal(dxa, dxb), "last block"
