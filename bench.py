@@ -69,6 +69,9 @@ def parse():
     p.add_argument("--roofline-steps", type=int, default=2, help="serialised steps timed per launch for the roofline")
     p.add_argument("--no-batch-losses", action="store_true",
                    help="run the original image's loss-network forwards separately (on the side stream)")
+    p.add_argument("--schedule", default="prefetch", choices=["pair", "prefetch"],
+                   help="stream schedule: pair = original synthesis beside the edited one; prefetch = the next "
+                        "iteration's original synthesis on a third stream (DESIGN.md section 6b)")
     return p.parse_args()
 
 
@@ -248,7 +251,7 @@ def main():
     finder = DirectionFinder(G, styles, clip, IDLoss("a", device=dev, weights=None, impl=args.id_impl), resolution=args.resolution,
                              batch_size=args.batch, global_batch=args.batch * world.world_size, seed=0, world=world,
                              init_delta=initial_delta(0, 0.01), n_epochs=1000,
-                             batch_losses=not args.no_batch_losses)
+                             batch_losses=not args.no_batch_losses, prefetch_orig=args.schedule != "pair")
     for _ in range(args.warmup):
         finder.step()
     torch.cuda.synchronize()
