@@ -128,6 +128,21 @@ int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w, float*
                       const smc_conv_phase* phases, int nphases, const float* s_in, const smc_conv_epilogue* epi,
                       float* workspace, int64_t workspace_bytes, void* stream);
 
+/* Winograd F(2x2, 3x3) form of the 3x3 stride-1 pad-1 convolution (the SynthesisLayer conv1 forward and its
+ * data gradient -- the one-phase smc_conv_gemm_f32 call with taps (dy, dx) in {-1,0,1}^2), same operands and
+ * epilogue semantics (modes STORE / MODACT / PRELU / PRELU_GRAD / AFFINE, no split-K workspace):
+ *   acc[n,o,y,x] = sum_{c,dy,dx} W[o][c][dy+1][dx+1] * s[n,c] * x[n, c, y+dy, x+dx]
+ * uw holds the transformed taps written by smc_wino_weights_f32 (flip 0 for this forward form).
+ * smc_conv3x3_wino_supported() says whether a shape has a kernel (cin % 8, cout % 32, w % 4 == 0, w >= 32,
+ * h even, input < 2 GiB); unsupported shapes return SMC_ERR_UNSUPPORTED. */
+int smc_conv3x3_wino_supported(int n, int cin, int cout, int h, int w);
+int smc_conv3x3_wino_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
+                         const float* s_in, const smc_conv_epilogue* epi, void* stream);
+/* w [cout][cin][3][3] -> uw [K][4][N][4] floats (16 * cin * cout, 16-B aligned), U = G g G^T per (k, n):
+ * flip = 0: K = cin, N = cout, g = w[n][k] (the forward correlation);
+ * flip = 1: K = cout, N = cin, g = w[k][n] rotated 180 degrees (the data gradient, conv^T). */
+int smc_wino_weights_f32(const float* w, int cout, int cin, int flip, float* uw, void* stream);
+
 /* Apply the modconv epilogue to a raw accumulator tensor, summing `nsplit` partial planes
  * (src + k*split_stride).  src/y/u_save: [n, c, h, w]. */
 int smc_modconv_epilogue_f32(const float* src, int nsplit, int64_t split_stride, float* y, int n, int c, int h,

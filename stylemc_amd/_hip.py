@@ -56,6 +56,9 @@ _SIGS = {
     "smc_conv_gemm_workspace_size": (c_int64, [c_int, c_int, c_int, c_int, c_int, P, c_int]),
     "smc_conv_gemm_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, c_int64,
                                   P]),
+    "smc_conv3x3_wino_supported": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "smc_conv3x3_wino_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P]),
+    "smc_wino_weights_f32": (c_int, [P, c_int, c_int, c_int, P, P]),
     "smc_modconv_epilogue_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, P, P]),
     "smc_modconv_blur_act_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                          c_int, c_int, c_int, c_int, c_float, c_int, P, P]),

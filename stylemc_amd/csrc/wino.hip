@@ -1,0 +1,367 @@
+// Winograd F(2x2, 3x3) convolution on fp32 MFMA for gfx950 (v_mfma_f32_16x16x4_f32).
+//
+// The 3x3 stride-1 'same' convolutions of the synthesis (every SynthesisLayer conv1 forward and its data
+// gradient, conv2d_resample.py:147-154 with groups = batch in the reference) are the largest GEMM family
+// of a find_direction step.  F(2x2, 3x3) computes each 2x2 output tile from a 4x4 input patch with 16
+// multiplies per (input, output) channel pair instead of 36 (2.25x fewer MFMA FLOPs):
+//     V = B^T d B   (input patch d, 4x4)          U = G g G^T   (3x3 taps g, frozen: smc_wino_weights_f32)
+//     M[xi] = sum_c U[xi][c][o] * V[xi][c][t]      (16 independent GEMMs, xi = 4a + b, on the matrix core)
+//     Y = A^T M A   (2x2 outputs)
+// B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1], G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1], A^T = [1 1 1 0; 0 1 -1 -1].
+// Everything stays fp32 (transforms on the VALU, products and sums on the f32-input MFMA); the transforms
+// add a few ulps next to the direct conv (tests/test_gpu_wino.py states the tolerance against fp64).
+//
+// Work decomposition (256 threads = 4 waves, 2 workgroups per CU):
+//   * a workgroup owns 32 output channels x 64 tiles (a TR x TC block of one image, TC = min(64, W/2)),
+//     each wave 32 channels x 16 tiles, all 16 xi: 16 x 2 accumulators of the 16x16x4 MFMA (128 registers).
+//     In the MFMA C layout a lane holds column j = tile and rows i = channels, so the 16 M values of one
+//     (channel, tile) sit in ONE lane (the same register of the 16 xi accumulators): the output transform
+//     and the modconv epilogue are lane-local.
+//   * K steps of 8 input channels; per step both operands go global -> LDS by DMA into a 2-stage ring (one
+//     barrier per step): the raw input rows of the block's (2TR+2) x (2TC+2) patch, staged from column
+//     2*tx0 - 4 as 16-B chunks (the buffer range check zero-fills the image border), and the U slab
+//     [8][4][32][4] (channel, xi group, out channel, xi % 4) by global_load_lds_dwordx4.
+//   * per k-quad (4 channels: MFMA k = lane >> 4) every lane reads ITS tile's 4x4 patch of ITS channel from
+//     LDS, transforms it in registers (32 adds; x s[n, c] for the style-scaled forward) and that is its B
+//     fragment for all 16 xi -- V never goes through LDS.  A fragments: 8 ds_read_b128 (bank-conflict free).
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int WBK = 8;    // input channels per K step
+constexpr int WBO = 32;   // output channels per workgroup
+constexpr int WBT = 64;   // tiles per workgroup (4 waves x 16)
+constexpr int WNT = 256;
+
+struct WinoParams {
+    const float* x;
+    int n, cin, h, w;
+    float* y;
+    int cout;
+    const float* uw;  // [cin][4][cout][4]
+    const float* s;   // [n][cin] or NULL
+    int mode;
+    const float* d;
+    const float* noise;
+    int64_t noise_nstride;
+    const float* noise_strength;
+    const float* bias;
+    int act;
+    float alpha, gain, clamp;
+    float* u_save;
+    smc::EpiExt ext;
+    int gx, gy;  // tile groups per image along x / y
+    int ntn;     // output-channel blocks (cout / 32)
+};
+
+template <int TC>
+struct WinoCfg {
+    static constexpr int TR = WBT / TC;             // tile rows of the block
+    static constexpr int ROWS = 2 * TR + 2;         // staged input rows
+    static constexpr int CH = TC / 2 + 2;           // 16-B chunks per staged row (2 TC + 8 floats)
+    static constexpr int PITCH = 4 * CH;
+    static constexpr int SLAB = ROWS * PITCH;       // floats per channel
+    static constexpr int PL = WBK * ROWS * CH;      // DMA lanes of the patch
+    static constexpr int PJ = (PL + 63) / 64;       // patch DMA wave-instructions per step
+    static constexpr int PF = PJ * 256;             // floats reserved for the patch (whole instructions)
+    static constexpr int UF = WBK * 16 * WBO;       // floats of the U slab
+    static constexpr int UJ = UF / 256;             // U DMA wave-instructions per step (16 B per lane)
+    static constexpr int STAGE = UF + PF;
+    static_assert(UJ % 4 == 0, "U slab splits evenly over the 4 waves");
+};
+
+template <int N>
+__device__ __forceinline__ void wino_wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int TC>
+__global__ __launch_bounds__(WNT, 2) void wino_kernel(WinoParams p) {
+    using C = WinoCfg<TC>;
+    constexpr int TR = C::TR, ROWS = C::ROWS, CH = C::CH, PITCH = C::PITCH, SLAB = C::SLAB, STAGE = C::STAGE;
+    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int H = p.h, W = p.w;
+
+    // XCD-aware bijective order (conv_gemm.hip): consecutive ids land on one XCD, output-channel blocks fastest,
+    // so the workgroups that stage the same input patch share an L2.
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int ob = wgid % p.ntn;
+    const int tg = wgid / p.ntn;
+    const int per_img = p.gx * p.gy;
+    const int nn = tg / per_img;
+    if (nn >= p.n) return;
+    const int rem = tg - nn * per_img;
+    const int ty0 = (rem / p.gx) * TR, tx0 = (rem % p.gx) * TC;
+    const int o0 = ob * WBO;
+
+    const int64_t plane = (int64_t)H * W;
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * plane * 4), 0x00020000);
+    const int nsteps = p.cin / WBK;
+
+    auto issue = [&](int ks, int slot) {
+        const int ci0 = ks * WBK;
+        float* us = smem + slot * STAGE;
+        // U slab: wave-instruction q covers runs 2q, 2q + 1 (run = channel * 4 + xi group: 32 x 16 B)
+#pragma unroll
+        for (int j = 0; j < C::UJ / 4; ++j) {
+            const int q = wave + 4 * j;
+            const int run = 2 * q + (lane >> 5);
+            const float* src = p.uw + (((int64_t)(ci0 + (run >> 2)) * 4 + (run & 3)) * p.cout + o0 + (lane & 31)) * 4;
+            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(us + q * 256),
+                                             16, 0, 0);
+        }
+        float* ps = us + C::UF;
+#pragma unroll
+        for (int j = wave; j < C::PJ; j += 4) {
+            const int L = j * 64 + lane;
+            const int c = L / (ROWS * CH);
+            const int r2 = L - c * (ROWS * CH);
+            const int r = r2 / CH, ch = r2 - r * CH;
+            const int gyy = 2 * ty0 - 1 + r, gxx = 2 * tx0 - 4 + 4 * ch;
+            const bool ok = c < WBK && gyy >= 0 && gyy < H && gxx >= 0 && gxx < W;
+            const int v = (int)((((int64_t)(nn * p.cin + ci0 + c) * H + gyy) * W + gxx) * 4);
+            const int msk = -(int)ok;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (__attribute__((address_space(3))) void*)(ps + j * 256),
+                                                     16, (v & msk) | (0x7ffffff0 & ~msk), 0, 0, 0);
+        }
+    };
+
+    f32x4 acc[16][2];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[xi][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int kq_lane = lane >> 4;   // MFMA k (channel within a k-quad)
+    const int tl = 16 * wave + (lane & 15);
+    const int tr = tl / TC, tc = tl - tr * TC;
+    const int poff = kq_lane * SLAB + 2 * tr * PITCH + 2 * tc + 3;
+    const int uoff = (kq_lane * 4 * WBO + (lane & 15)) * 4;
+    const bool has_s = p.s != nullptr;
+    const float* srow = has_s ? p.s + (int64_t)nn * p.cin + kq_lane : p.x;
+    float sv[2] = {1.f, 1.f}, sn[2] = {1.f, 1.f};
+
+    if (nsteps > 0) {
+        issue(0, 0);
+        if (has_s) { sn[0] = srow[0]; sn[1] = srow[4]; }
+    }
+    for (int ks = 0; ks < nsteps; ++ks) {
+        wino_wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // step ks landed for every wave; the other slot is free
+        asm volatile("" ::: "memory");
+        sv[0] = sn[0]; sv[1] = sn[1];
+        if (ks + 1 < nsteps) {
+            issue(ks + 1, (ks + 1) & 1);
+            if (has_s) { sn[0] = srow[(ks + 1) * WBK]; sn[1] = srow[(ks + 1) * WBK + 4]; }
+        }
+        const float* us = smem + (ks & 1) * STAGE;
+        const float* ps = us + C::UF;
+#pragma unroll
+        for (int kq = 0; kq < 2; ++kq) {
+            const float* pp = ps + kq * 4 * SLAB + poff;
+            float dd[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) dd[i][j] = pp[i * PITCH + j];
+            f32x4 a[4][2];
+            const float* up = us + kq * 4 * 4 * WBO * 4 + uoff;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) a[g][b] = *reinterpret_cast<const f32x4*>(up + (g * WBO + 16 * b) * 4);
+            // V = B^T d B (rows, then columns), scaled by s[n, c]
+            float t[4][4], v[16];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                t[0][j] = dd[0][j] - dd[2][j];
+                t[1][j] = dd[1][j] + dd[2][j];
+                t[2][j] = dd[2][j] - dd[1][j];
+                t[3][j] = dd[1][j] - dd[3][j];
+            }
+            const float sc = sv[kq];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                v[4 * i + 0] = (t[i][0] - t[i][2]) * sc;
+                v[4 * i + 1] = (t[i][1] + t[i][2]) * sc;
+                v[4 * i + 2] = (t[i][2] - t[i][1]) * sc;
+                v[4 * i + 3] = (t[i][1] - t[i][3]) * sc;
+            }
+#pragma unroll
+            for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[xi][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[xi >> 2][b][xi & 3], v[xi], acc[xi][b], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's reads are done before the next barrier
+    }
+
+    // ---- epilogue: Y = A^T M A per (channel, tile), then the conv epilogue (smc::epi_y / epi_ext_apply)
+    const int yy0 = 2 * (ty0 + tr), xx0 = 2 * (tx0 + tc);
+    const float nstr = p.noise_strength ? *p.noise_strength : 1.f;
+    float nz[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    if (p.mode == SMC_EPI_MODACT && p.noise) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) nz[i][j] = p.noise[nn * p.noise_nstride + (int64_t)(yy0 + i) * W + xx0 + j] * nstr;
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int o = o0 + 16 * b + 4 * kq_lane + r;
+            float m[4][4];
+#pragma unroll
+            for (int xi = 0; xi < 16; ++xi) m[xi >> 2][xi & 3] = acc[xi][b][r];
+            float rr[2][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                rr[0][j] = m[0][j] + m[1][j] + m[2][j];
+                rr[1][j] = m[1][j] - m[2][j] - m[3][j];
+            }
+            float out[2][2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                out[i][0] = rr[i][0] + rr[i][1] + rr[i][2];
+                out[i][1] = rr[i][1] - rr[i][2] - rr[i][3];
+            }
+            const int64_t obase = ((int64_t)nn * p.cout + o) * plane;
+            if (p.mode == SMC_EPI_MODACT) {
+                const float dsc = (p.d ? p.d[(int64_t)nn * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
+                const float bo = p.bias ? p.bias[o] : 0.f;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int64_t idx = obase + (int64_t)(yy0 + i) * W + xx0;
+                    if (p.u_save) *reinterpret_cast<float2*>(p.u_save + idx) = make_float2(out[i][0], out[i][1]);
+                    float q[2];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        q[j] = smc::epi_y(out[i][j], dsc, nz[i][j], bo, p.act, p.alpha, p.gain, p.clamp);
+                        if (p.ext.residual)
+                            q[j] = smc::epi_ext_apply(SMC_EPI_STORE, q[j], nn, o, idx + j, yy0 + i, xx0 + j, p.cout, H, W,
+                                                      nullptr, nullptr, p.ext);
+                    }
+                    *reinterpret_cast<float2*>(p.y + idx) = make_float2(q[0], q[1]);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int64_t idx = obase + (int64_t)(yy0 + i) * W + xx0;
+                    float q[2];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        q[j] = smc::epi_ext_apply(p.mode, out[i][j], nn, o, idx + j, yy0 + i, xx0 + j, p.cout, H, W, p.bias,
+                                                  p.u_save, p.ext);
+                    *reinterpret_cast<float2*>(p.y + idx) = make_float2(q[0], q[1]);
+                }
+            }
+        }
+    }
+}
+
+// U = G g G^T per (k, n): flip = 0: g = w[n][k] (k = cin, n = cout: the forward correlation);
+// flip = 1: g = w[k][n] rotated by 180 degrees (k = cout, n = cin: the data gradient).  Out: [K][4][N][4].
+__global__ __launch_bounds__(256) void wino_weights_kernel(const float* w, int cout, int cin, int flip, float* uw) {
+    const int K = flip ? cout : cin, N = flip ? cin : cout;
+    const int64_t total = (int64_t)K * N;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(e / N), nidx = (int)(e - (int64_t)k * N);
+        float g[3][3];
+        const float* src = flip ? w + ((int64_t)k * cin + nidx) * 9 : w + ((int64_t)nidx * cin + k) * 9;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) g[i][j] = flip ? src[(2 - i) * 3 + (2 - j)] : src[i * 3 + j];
+        float gg[4][3];  // G g
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            gg[0][j] = g[0][j];
+            gg[1][j] = 0.5f * (g[0][j] + g[1][j] + g[2][j]);
+            gg[2][j] = 0.5f * (g[0][j] - g[1][j] + g[2][j]);
+            gg[3][j] = g[2][j];
+        }
+        float u[4][4];   // (G g) G^T
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            u[i][0] = gg[i][0];
+            u[i][1] = 0.5f * (gg[i][0] + gg[i][1] + gg[i][2]);
+            u[i][2] = 0.5f * (gg[i][0] - gg[i][1] + gg[i][2]);
+            u[i][3] = gg[i][2];
+        }
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi) uw[(((int64_t)k * 4 + (xi >> 2)) * N + nidx) * 4 + (xi & 3)] = u[xi >> 2][xi & 3];
+    }
+}
+
+int wino_tc(int h, int w) {
+    if (h % 2 || w % 4 || w < 32) return 0;
+    const int tc = w / 2 >= 64 ? 64 : w / 2;
+    if ((w / 2) % tc || (h / 2) % (WBT / tc)) return 0;
+    return tc;
+}
+
+}  // namespace
+
+SMC_API int smc_conv3x3_wino_supported(int n, int cin, int cout, int h, int w) {
+    if (n < 1 || cin < WBK || cin % WBK || cout < WBO || cout % WBO) return 0;
+    if ((int64_t)n * cin * h * w * 4 >= (1LL << 31)) return 0;  // raw buffer offsets are 32-bit
+    return wino_tc(h, w) != 0;
+}
+
+SMC_API int smc_wino_weights_f32(const float* w, int cout, int cin, int flip, float* uw, void* stream) {
+    SMC_CHECK(w && uw && cout >= 1 && cin >= 1, "smc_wino_weights_f32: bad arguments");
+    SMC_CHECK((reinterpret_cast<uintptr_t>(uw) & 15) == 0, "smc_wino_weights_f32: uw must be 16-B aligned");
+    const int64_t total = (int64_t)cout * cin;
+    hipLaunchKernelGGL(wino_weights_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(total, 256), 4096)),
+                       dim3(256), 0, smc::as_stream(stream), w, cout, cin, flip, uw);
+    return smc::check_launch("smc_wino_weights_f32");
+}
+
+SMC_API int smc_conv3x3_wino_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
+                                 const float* s_in, const smc_conv_epilogue* epi, void* stream) {
+    SMC_CHECK(x && y && uw, "smc_conv3x3_wino_f32: null pointer");
+    if (!smc_conv3x3_wino_supported(n, cin, cout, h, w)) {
+        smc::set_error("smc_conv3x3_wino_f32: no Winograd kernel for n=%d cin=%d cout=%d %dx%d", n, cin, cout, h, w);
+        return SMC_ERR_UNSUPPORTED;
+    }
+    SMC_CHECK((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 7) == 0 &&
+                  (reinterpret_cast<uintptr_t>(uw) & 15) == 0,
+              "smc_conv3x3_wino_f32: x / uw must be 16-B and y 8-B aligned");
+    smc_conv_epilogue e{};
+    e.mode = SMC_EPI_STORE; e.act = SMC_ACT_LINEAR; e.gain = 1.f; e.clamp = -1.f;
+    if (epi) e = *epi;
+    SMC_CHECK(e.mode >= SMC_EPI_STORE && e.mode <= SMC_EPI_AFFINE, "smc_conv3x3_wino_f32: bad epilogue mode %d", e.mode);
+    SMC_CHECK((e.mode != SMC_EPI_PRELU && e.mode != SMC_EPI_PRELU_GRAD) || e.alpha_c,
+              "smc_conv3x3_wino_f32: PReLU epilogue needs alpha_c");
+    SMC_CHECK(e.mode != SMC_EPI_PRELU_GRAD || e.act_ref, "smc_conv3x3_wino_f32: PRELU_GRAD needs act_ref");
+    SMC_CHECK(!e.u_save || (reinterpret_cast<uintptr_t>(e.u_save) & 7) == 0, "smc_conv3x3_wino_f32: u_save alignment");
+    WinoParams p{};
+    p.x = x; p.n = n; p.cin = cin; p.h = h; p.w = w; p.y = y; p.cout = cout; p.uw = uw; p.s = s_in;
+    p.mode = e.mode; p.d = e.d; p.noise = e.noise; p.noise_nstride = e.noise_nstride;
+    p.noise_strength = e.noise_strength; p.bias = e.bias; p.act = e.act; p.alpha = e.alpha; p.gain = e.gain;
+    p.clamp = e.clamp; p.u_save = e.u_save;
+    p.ext = smc::epi_ext(epi);
+    const int tc = wino_tc(h, w);
+    p.gx = (w / 2) / tc;
+    p.gy = (h / 2) / (WBT / tc);
+    p.ntn = cout / WBO;
+    const int64_t wgs = (int64_t)n * p.gx * p.gy * p.ntn;
+    SMC_CHECK(wgs < (1LL << 31), "smc_conv3x3_wino_f32: grid too large");
+    hipStream_t st = smc::as_stream(stream);
+    if (tc == 64) hipLaunchKernelGGL(wino_kernel<64>, dim3((unsigned)wgs), dim3(WNT), 0, st, p);
+    else if (tc == 32) hipLaunchKernelGGL(wino_kernel<32>, dim3((unsigned)wgs), dim3(WNT), 0, st, p);
+    else hipLaunchKernelGGL(wino_kernel<16>, dim3((unsigned)wgs), dim3(WNT), 0, st, p);
+    return smc::check_launch("smc_conv3x3_wino_f32");
+}

@@ -64,6 +64,18 @@ class PackedConv:
                     self.phases.append((py, px, [(-(ky - py) // 2, -(kx - px) // 2) for ky, kx in sel], wk))
             self.bwd_taps = [(ky, kx) for ky, kx in taps]  # stride-2 gather over dT
         self._cache = {}
+        self._wino = {}
+
+    def wino_weights(self, flip):
+        """Winograd F(2x2, 3x3) transformed taps (smc_wino_weights_f32) of the 3x3 'same' conv, built once on the
+        weights' device: flip 0 = the forward, 1 = the data gradient."""
+        if flip not in self._wino:
+            W = self.wk_bwd  # [t][o][i] -> back to [o][i][3][3] on the same device
+            w = W.reshape(3, 3, self.cout, self.cin).permute(2, 3, 0, 1).contiguous()
+            uw = torch.empty(16 * self.cin * self.cout, device=w.device, dtype=torch.float32)
+            _hip.call("smc_wino_weights_f32", w.data_ptr(), self.cout, self.cin, flip, uw.data_ptr(), _hip.stream())
+            self._wino[flip] = uw
+        return self._wino[flip]
 
     def fwd_phases(self, h, w):
         key = ("f", h, w)
@@ -105,6 +117,31 @@ def gemm(x, y, phases, nph, cin, cout, s=None, epi=None, alg_flops=0.0, alg_byte
               _hip.ptr(s), ctypes.byref(epi) if epi is not None else None, _hip.ptr(ws), ws_bytes, _hip.stream())
     if tok is not None:
         tm.finish(tok)
+
+
+# Winograd F(2x2, 3x3) for the 3x3 stride-1 convs wherever smc_conv3x3_wino_supported() has a kernel (module
+# switch, not an environment knob: tests / tools flip it to compare against the direct implicit GEMM).
+WINOGRAD = True
+
+
+def wino_ok(n, cin, cout, h, w):
+    return WINOGRAD and bool(_hip.load().smc_conv3x3_wino_supported(n, cin, cout, h, w))
+
+
+def wino(x, y, uw, cin, cout, s=None, epi=None, alg_flops=0.0, alg_bytes=0):
+    """One smc_conv3x3_wino_f32 launch (3x3, stride 1, pad 1).  alg_flops: the MFMA FLOPs it executes
+    (16 / 36 of the direct conv's)."""
+    n, _, h, w = x.shape
+    tm = _hip.timer()
+    tok = tm.wrap(alg_flops, alg_bytes) if tm is not None else None
+    _hip.call("smc_conv3x3_wino_f32", x.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(), _hip.ptr(s),
+              ctypes.byref(epi) if epi is not None else None, _hip.stream())
+    if tok is not None:
+        tm.finish(tok)
+
+
+def wino_flops(n, cin, cout, h, w):
+    return 2.0 * n * cin * cout * (h // 2) * (w // 2) * 16
 
 
 def _epilogue(mode, d=None, noise=None, noise_nstride=0, strength=None, bias=None, act="linear", alpha=0.0,
@@ -169,7 +206,10 @@ def _modconv_fwd(ctx, x, styles, spec, noise, strength, gain, clamp, need_dx, ne
     epi = _epilogue(_hip.EPI_MODACT, d, nz, nstride, strength, spec.bias, spec.act, spec.alpha, gain, clamp, u)
     phases, nph, th, tw = P.fwd_phases(h, w)
     wbytes = 4 * P.k * P.k * cin * P.cout
-    if spec.up == 1:
+    if spec.up == 1 and P.k == 3 and wino_ok(n, cin, P.cout, h, w):
+        wino(x, y, P.wino_weights(0), cin, P.cout, s=styles, epi=epi, alg_flops=wino_flops(n, cin, P.cout, h, w),
+             alg_bytes=4 * x.numel() + 4 * y.numel() * (2 if u is not None else 1) + 16 * 4 * cin * P.cout)
+    elif spec.up == 1:
         gemm(x, y, phases, nph, cin, P.cout, s=styles, epi=epi,
              alg_flops=conv_flops(n, cin, P.cout, r_h, r_w, P.k * P.k),
              alg_bytes=4 * x.numel() + 4 * y.numel() * (2 if u is not None else 1) + wbytes)
@@ -234,10 +274,15 @@ def _modconv_bwd(ctx, saved, gy, need_dx, need_ds, g=None):
     else:
         ebw = _epilogue(_hip.EPI_STORE)
         out = dxs
-    phases, nph = P.bwd_phases(h, w)
     g_bytes = 4 * g.numel() if spec.up == 1 else 4 * n * P.cout * (2 * h + 1) * (2 * w + 1)
-    gemm(g, out, phases, nph, P.cout, cin, epi=ebw, alg_flops=conv_flops(n, P.cout, cin, h, w, P.k * P.k),
-         alg_bytes=g_bytes + 4 * out.numel() * (2 if (need_dx and need_ds) else 1) + 4 * P.k * P.k * cin * P.cout)
+    out_bytes = 4 * out.numel() * (2 if (need_dx and need_ds) else 1)
+    if spec.up == 1 and P.k == 3 and wino_ok(n, P.cout, cin, h, w):
+        wino(g, out, P.wino_weights(1), P.cout, cin, epi=ebw, alg_flops=wino_flops(n, P.cout, cin, h, w),
+             alg_bytes=g_bytes + out_bytes + 16 * 4 * cin * P.cout)
+    else:
+        phases, nph = P.bwd_phases(h, w)
+        gemm(g, out, phases, nph, P.cout, cin, epi=ebw, alg_flops=conv_flops(n, P.cout, cin, h, w, P.k * P.k),
+             alg_bytes=g_bytes + out_bytes + 4 * P.k * P.k * cin * P.cout)
     ds = None
     if need_ds:
         ds = torch.empty(n, cin, device=x.device, dtype=torch.float32)

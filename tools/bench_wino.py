@@ -1,0 +1,72 @@
+"""Winograd F(2x2, 3x3) vs the direct implicit GEMM on the synthesis conv1 shapes (FFHQ-1024, batch 4).
+
+    python tools/bench_wino.py [--batch 4] [--reps 10]
+Per shape: us per launch of each path, the direct-equivalent TFLOP/s (dense 3x3 MACs x 2 / time) and the Winograd
+kernel's MFMA fraction (its own 16-multiply FLOPs / time vs 157.3 TF/s).
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from stylemc_amd import _hip, build, modconv  # noqa: E402
+
+PEAK = 157.3e12
+
+
+def timeit(fn, reps):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1e-3 / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    build.build(verbose=False)
+    n, dev = args.batch, "cuda"
+    tot = {"direct": 0.0, "wino": 0.0}
+    for r in [32, 64, 128, 256, 512, 1024]:
+        c = min(32768 // r, 512)
+        W = torch.randn(c, c, 3, 3, device=dev) / (3 * c ** 0.5)
+        P = modconv.PackedConv(W, 1)
+        x = torch.randn(n, c, r, r, device=dev)
+        s = torch.rand(n, c, device=dev) + 0.5
+        y = torch.empty_like(x)
+        phases, nph, _, _ = P.fwd_phases(r, r)
+        bph, bnph = P.bwd_phases(r, r)
+        uf, ub = P.wino_weights(0), P.wino_weights(1)
+        st = modconv._epilogue(_hip.EPI_STORE)
+        runs = {
+            ("fwd", "direct"): lambda: modconv.gemm(x, y, phases, nph, c, c, s=s, epi=st),
+            ("fwd", "wino"): lambda: modconv.wino(x, y, uf, c, c, s=s, epi=st),
+            ("bwd", "direct"): lambda: modconv.gemm(x, y, bph, bnph, c, c, epi=st),
+            ("bwd", "wino"): lambda: modconv.wino(x, y, ub, c, c, epi=st),
+        }
+        flops = modconv.conv_flops(n, c, c, r, r, 9)
+        wfl = modconv.wino_flops(n, c, c, r, r)
+        for kind in ("fwd", "bwd"):
+            td = timeit(runs[(kind, "direct")], args.reps)
+            tw = timeit(runs[(kind, "wino")], args.reps)
+            tot["direct"] += td
+            tot["wino"] += tw
+            print(f"r={r:5d} c={c:4d} {kind}: direct {td * 1e6:8.1f} us ({flops / td / 1e12:6.1f} TF/s, "
+                  f"{flops / td / PEAK:.3f})  wino {tw * 1e6:8.1f} us (eq {flops / tw / 1e12:6.1f} TF/s, "
+                  f"MFMA frac {wfl / tw / PEAK:.3f})  speedup {td / tw:.2f}x", flush=True)
+    print(f"total: direct {tot['direct'] * 1e3:.3f} ms, wino {tot['wino'] * 1e3:.3f} ms, "
+          f"speedup {tot['direct'] / tot['wino']:.2f}x")
+
+
+if __name__ == "__main__":
+    main()
