@@ -14,10 +14,11 @@ per step).  value = images/s = 2 x seeds/s (edited + original
 image per seed), seeds counted exactly (the batch picker can draw the short
 last batch of the 129 seeds).
 
-roofline: the dominant kernel family, the synthesis modconv GEMMs (``conv_gemm_lds_kernel`` /
-``conv_gemm_kernel`` / ``convt_gemm_kernel``, every launch of smc_conv_gemm_f32 from modconv.py):
-algorithmic FLOPs of each launch (dense MACs x 2 of the conv it computes) / its
-duration, timed with HIP events around every launch during --roofline-steps extra steps run right
+roofline: the dominant kernel family, the synthesis convs (every smc_conv3x3_wino_f32 / smc_conv_gemm_f32 launch
+from modconv.py: ``wino_kernel`` for the 3x3 'same' convs, ``conv_gemm_lds_kernel`` / ``conv_row_kernel`` /
+``convt_lds_kernel`` ... for the rest): the MFMA FLOPs of each launch's algorithm (dense MACs x 2 for the direct
+kernels; 16 multiplies per 2x2 tile and channel pair for Winograd, reported beside the
+direct-equivalent rate) / its duration, timed with HIP events around every launch during --roofline-steps extra steps run right
 after the timed region with the original-image branch serialised onto the main stream (in the timed
 region that branch runs on a second stream, and a launch's event interval would include CU time
 taken by the other stream's kernels), against the fp32 MFMA peak (157.3 TFLOP/s,
@@ -288,12 +289,29 @@ def main():
         finder.overlap = True
         s = timer.summary()
         achieved = s["flops"] / s["seconds"] / 1e12 if s["seconds"] > 0 else 0.0
+
+        def part(d, what):
+            tf = d["flops"] / d["seconds"] / 1e12 if d["seconds"] > 0 else 0.0
+            return {"what": what, "launches": d["launches"], "ms_per_step": round(1e3 * d["seconds"] / args.roofline_steps, 3),
+                    "avg_launch_us": round(1e6 * d["seconds"] / max(d["launches"], 1), 2),
+                    "achieved": round(tf, 3), "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
+                    "direct_equiv_tflops": round(d["equiv_flops"] / d["seconds"] / 1e12, 3) if d["seconds"] > 0 else 0.0}
+
+        kinds = {
+            "wino": ("Winograd F(2x2,3x3) 3x3 'same' convs (conv1 fwd + data grad); FLOPs = its 16 multiplies "
+                            "per 2x2 tile and channel pair (4/9 of the direct conv's)"),
+            "direct": ("direct implicit-GEMM kernels (conv_gemm_lds / conv_row / convt_lds ...: transposed conv0, "
+                       "its stride-2 data grad, the < 32-px layers); FLOPs = dense MACs x 2"),
+        }
         roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),
-                    "kernel": "conv_gemm_kernel family (synthesis modconv GEMMs)", "launches": s["launches"],
+                    "kernel": "synthesis conv family (wino_kernel + the direct implicit-GEMM kernels)",
+                    "launches": s["launches"],
                     "avg_launch_us": round(1e6 * s["seconds"] / max(s["launches"], 1), 2),
                     "alg_gflop_per_launch": round(s["flops"] / max(s["launches"], 1) / 1e9, 3),
                     "alg_bytes_per_launch": int(s["bytes"] / max(s["launches"], 1)),
+                    "direct_equiv_tflops": round(s["equiv_flops"] / s["seconds"] / 1e12, 3) if s["seconds"] > 0 else 0.0,
+                    "parts": {k: part(s["kinds"][k], kinds.get(k, k)) for k in sorted(s["kinds"])},
                     "share_of_step_time": round(s["seconds"] / dt_r, 4),
                     "measured": f"HIP events around every launch, {args.roofline_steps} serialised steps after the "
                                 f"timed region"}

@@ -164,24 +164,32 @@ class KernelTimer:
 
     def __init__(self, family):
         self.family = family
-        self.records = []  # (start_event, end_event, flops, algorithmic bytes)
+        self.records = []  # (start_event, end_event, flops, algorithmic bytes, kind, direct-equivalent flops)
 
-    def wrap(self, flops, nbytes=0):
+    def wrap(self, flops, nbytes=0, kind="direct", equiv_flops=None):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
-        return s, e, flops, nbytes
+        return s, e, flops, nbytes, kind, flops if equiv_flops is None else equiv_flops
 
     def finish(self, token):
-        s, e, flops, nbytes = token
+        s, e, flops, nbytes, kind, eq = token
         e.record()
-        self.records.append((s, e, flops, nbytes))
+        self.records.append((s, e, flops, nbytes, kind, eq))
 
     def summary(self):
         torch.cuda.synchronize()
-        times = [r[0].elapsed_time(r[1]) * 1e-3 for r in self.records]
-        return {"launches": len(times), "seconds": sum(times), "flops": sum(r[2] for r in self.records),
-                "bytes": sum(r[3] for r in self.records)}
+        out = {"launches": 0, "seconds": 0.0, "flops": 0.0, "bytes": 0, "equiv_flops": 0.0, "kinds": {}}
+        for s, e, flops, nbytes, kind, eq in self.records:
+            t = s.elapsed_time(e) * 1e-3
+            for d in (out, out["kinds"].setdefault(kind, {"launches": 0, "seconds": 0.0, "flops": 0.0, "bytes": 0,
+                                                          "equiv_flops": 0.0})):
+                d["launches"] += 1
+                d["seconds"] += t
+                d["flops"] += flops
+                d["bytes"] += nbytes
+                d["equiv_flops"] += eq
+        return out
 
 
 _timer = None

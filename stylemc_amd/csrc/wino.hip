@@ -35,7 +35,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int WBK = 8;    // input channels per K step
 constexpr int WBO = 32;   // output channels per workgroup
 constexpr int WBT = 64;   // tiles per workgroup (4 waves x 16)
-constexpr int WNT = 256;
+constexpr int WOBW = 2;   // the library's waves-per-workgroup variant (wino_kernel OBW)
 
 struct WinoParams {
     const float* x;
@@ -79,9 +79,17 @@ __device__ __forceinline__ void wino_wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int TC>
-__global__ __launch_bounds__(WNT, 2) void wino_kernel(WinoParams p) {
+// PROBE (0 in the library) removes pieces for the timing probe tools/probes/wino_probe.hip: 1 the U DMAs after the
+// first step, 2 the patch DMAs after the first step, 4 the per-step wait + barrier, 8 the epilogue, 16 the transform,
+// 32 the LDS fragment reads.
+// OBW: 16-channel output blocks per wave (2: 4 waves of 32 channels x 16 tiles, 2 waves / SIMD; 1: 8 waves of
+// 16 channels x 16 tiles, 4 waves / SIMD -- both o-waves of a tile row transform the same patch).
+template <int TC, int OBW, int PROBE = 0>
+__global__ __launch_bounds__(64 * 8 / OBW) __attribute__((amdgpu_waves_per_eu(8 / (2 * OBW) * 1, 8 / (2 * OBW) * 1)))
+void wino_kernel(WinoParams p) {
     using C = WinoCfg<TC>;
+    constexpr int NW = 8 / OBW;      // waves per workgroup
+    constexpr int OW = 2 / OBW;      // o-waves per tile row of waves
     constexpr int TR = C::TR, ROWS = C::ROWS, CH = C::CH, PITCH = C::PITCH, SLAB = C::SLAB, STAGE = C::STAGE;
     __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
@@ -114,16 +122,18 @@ __global__ __launch_bounds__(WNT, 2) void wino_kernel(WinoParams p) {
         float* us = smem + slot * STAGE;
         // U slab: wave-instruction q covers runs 2q, 2q + 1 (run = channel * 4 + xi group: 32 x 16 B)
 #pragma unroll
-        for (int j = 0; j < C::UJ / 4; ++j) {
-            const int q = wave + 4 * j;
+        for (int j = 0; j < ((PROBE & 1) != 0 && ks > 0 ? 0 : C::UJ / NW); ++j) {
+            const int q = wave + NW * j;
             const int run = 2 * q + (lane >> 5);
             const float* src = p.uw + (((int64_t)(ci0 + (run >> 2)) * 4 + (run & 3)) * p.cout + o0 + (lane & 31)) * 4;
             __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(us + q * 256),
                                              16, 0, 0);
         }
+        if constexpr ((PROBE & 2) != 0)
+            if (ks > 0) return;
         float* ps = us + C::UF;
 #pragma unroll
-        for (int j = wave; j < C::PJ; j += 4) {
+        for (int j = wave; j < C::PJ; j += NW) {
             const int L = j * 64 + lane;
             const int c = L / (ROWS * CH);
             const int r2 = L - c * (ROWS * CH);
@@ -137,28 +147,88 @@ __global__ __launch_bounds__(WNT, 2) void wino_kernel(WinoParams p) {
         }
     };
 
-    f32x4 acc[16][2];
+    f32x4 acc[16][OBW];
 #pragma unroll
     for (int xi = 0; xi < 16; ++xi)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[xi][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int b = 0; b < OBW; ++b) acc[xi][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int kq_lane = lane >> 4;   // MFMA k (channel within a k-quad)
-    const int tl = 16 * wave + (lane & 15);
+    const int wo = wave % OW, wt = wave / OW;
+    const int ob16 = wo * OBW;       // first 16-channel block of this wave
+    const int tl = 16 * wt + (lane & 15);
     const int tr = tl / TC, tc = tl - tr * TC;
     const int poff = kq_lane * SLAB + 2 * tr * PITCH + 2 * tc + 3;
-    const int uoff = (kq_lane * 4 * WBO + (lane & 15)) * 4;
+    const int uoff = (kq_lane * 4 * WBO + 16 * ob16 + (lane & 15)) * 4;
     const bool has_s = p.s != nullptr;
     const float* srow = has_s ? p.s + (int64_t)nn * p.cin + kq_lane : p.x;
     float sv[2] = {1.f, 1.f}, sn[2] = {1.f, 1.f};
+
+    // Fragment pipeline.  A step's 8 MFMA groups gi = 4 kq + g (k-quad kq, xi group g: 8 MFMAs each) read their A
+    // fragments from a 2-deep register ring loaded one group ahead; the k-quad-1 patch is read under group 0 and
+    // transformed under group 3.  The last group of a step is deferred past the next step's barrier, so its MFMAs
+    // cover the LDS latency of the next step's first patch / A reads (it needs only registers).
+    float pd[16], va[16], vb[16];
+    f32x4 ar[2][OBW];
+    bool pend = false;
+    auto load_patch = [&](const float* ps, int kq) {
+        if constexpr ((PROBE & 32) != 0) return;
+        const float* pp = ps + kq * 4 * SLAB + poff;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pd[4 * i + j] = pp[i * PITCH + j];
+    };
+    auto load_a = [&](const float* us, int gi, f32x4 (&a)[OBW]) {
+        if constexpr ((PROBE & 32) != 0) {
+#pragma unroll
+            for (int b = 0; b < OBW; ++b) a[b] = f32x4{pd[gi], pd[gi + 1], pd[gi + 2], pd[b]};
+            return;
+        }
+        const float* up = us + (gi >> 2) * 4 * 4 * WBO * 4 + uoff + (gi & 3) * WBO * 4;
+#pragma unroll
+        for (int b = 0; b < OBW; ++b) a[b] = *reinterpret_cast<const f32x4*>(up + 16 * 4 * b);
+    };
+    // V = B^T d B (rows, then columns), scaled by s[n, c]
+    auto transform = [&](float sc, float (&v)[16]) {
+        if constexpr ((PROBE & 16) != 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = pd[i];
+            return;
+        }
+        float t[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            t[0][j] = pd[j] - pd[8 + j];
+            t[1][j] = pd[4 + j] + pd[8 + j];
+            t[2][j] = pd[8 + j] - pd[4 + j];
+            t[3][j] = pd[4 + j] - pd[12 + j];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[4 * i + 0] = (t[i][0] - t[i][2]) * sc;
+            v[4 * i + 1] = (t[i][1] + t[i][2]) * sc;
+            v[4 * i + 2] = (t[i][2] - t[i][1]) * sc;
+            v[4 * i + 3] = (t[i][1] - t[i][3]) * sc;
+        }
+    };
+    auto mma_group = [&](int g, const f32x4 (&a)[OBW], const float (&v)[16]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int b = 0; b < OBW; ++b)
+                acc[4 * g + j][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[b][j], v[4 * g + j], acc[4 * g + j][b], 0, 0, 0);
+    };
 
     if (nsteps > 0) {
         issue(0, 0);
         if (has_s) { sn[0] = srow[0]; sn[1] = srow[4]; }
     }
     for (int ks = 0; ks < nsteps; ++ks) {
-        wino_wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();  // step ks landed for every wave; the other slot is free
+        if constexpr ((PROBE & 4) == 0) {
+            wino_wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();  // step ks landed for every wave; slot (ks + 1) & 1 is no longer read
+        }
         asm volatile("" ::: "memory");
         sv[0] = sn[0]; sv[1] = sn[1];
         if (ks + 1 < nsteps) {
@@ -167,47 +237,50 @@ __global__ __launch_bounds__(WNT, 2) void wino_kernel(WinoParams p) {
         }
         const float* us = smem + (ks & 1) * STAGE;
         const float* ps = us + C::UF;
+        // (sched_barrier fences keep each phase where it is written: the compiler would otherwise sink the
+        // prefetches next to their use to save registers and wait on them with lgkmcnt(0))
+        load_patch(ps, 0);
+        load_a(us, 0, ar[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (pend) mma_group(3, ar[1], vb);  // the previous step's last group
+        __builtin_amdgcn_sched_barrier(0);
+        transform(sv[0], va);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kq = 0; kq < 2; ++kq) {
-            const float* pp = ps + kq * 4 * SLAB + poff;
-            float dd[4][4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) dd[i][j] = pp[i * PITCH + j];
-            f32x4 a[4][2];
-            const float* up = us + kq * 4 * 4 * WBO * 4 + uoff;
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-#pragma unroll
-                for (int b = 0; b < 2; ++b) a[g][b] = *reinterpret_cast<const f32x4*>(up + (g * WBO + 16 * b) * 4);
-            // V = B^T d B (rows, then columns), scaled by s[n, c]
-            float t[4][4], v[16];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                t[0][j] = dd[0][j] - dd[2][j];
-                t[1][j] = dd[1][j] + dd[2][j];
-                t[2][j] = dd[2][j] - dd[1][j];
-                t[3][j] = dd[1][j] - dd[3][j];
+        for (int gi = 0; gi < 8; ++gi) {
+            if (gi + 1 < 8) load_a(us, gi + 1, ar[(gi + 1) & 1]);
+            if (gi == 0) load_patch(ps, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (gi < 7) {
+                mma_group(gi & 3, ar[gi & 1], gi < 4 ? va : vb);
+            } else {
+                pend = ks + 1 < nsteps;
+                if (!pend) mma_group(3, ar[1], vb);
             }
-            const float sc = sv[kq];
+            if (gi == 3) {
+                transform(sv[1], vb);
+                // the transform's VALU ops between this group's MFMAs (the MFMA pipe stays fed)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                v[4 * i + 0] = (t[i][0] - t[i][2]) * sc;
-                v[4 * i + 1] = (t[i][1] + t[i][2]) * sc;
-                v[4 * i + 2] = (t[i][2] - t[i][1]) * sc;
-                v[4 * i + 3] = (t[i][1] - t[i][3]) * sc;
+                for (int q = 0; q < 4 * OBW; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 12 / OBW, 0);
+                }
             }
-#pragma unroll
-            for (int xi = 0; xi < 16; ++xi)
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-                    acc[xi][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[xi >> 2][b][xi & 3], v[xi], acc[xi][b], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's reads are done before the next barrier
     }
 
     // ---- epilogue: Y = A^T M A per (channel, tile), then the conv epilogue (smc::epi_y / epi_ext_apply)
+    if constexpr ((PROBE & 8) != 0) {
+        float sum = 0.f;
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+            for (int b = 0; b < OBW; ++b) sum += acc[xi][b][0] + acc[xi][b][1] + acc[xi][b][2] + acc[xi][b][3];
+        if (sum == 12345.f) p.y[tid] = sum;
+        return;
+    }
     const int yy0 = 2 * (ty0 + tr), xx0 = 2 * (tx0 + tc);
     const float nstr = p.noise_strength ? *p.noise_strength : 1.f;
     float nz[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
@@ -218,10 +291,10 @@ __global__ __launch_bounds__(WNT, 2) void wino_kernel(WinoParams p) {
             for (int j = 0; j < 2; ++j) nz[i][j] = p.noise[nn * p.noise_nstride + (int64_t)(yy0 + i) * W + xx0 + j] * nstr;
     }
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < OBW; ++b) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int o = o0 + 16 * b + 4 * kq_lane + r;
+            const int o = o0 + 16 * (ob16 + b) + 4 * kq_lane + r;
             float m[4][4];
 #pragma unroll
             for (int xi = 0; xi < 16; ++xi) m[xi >> 2][xi & 3] = acc[xi][b][r];
@@ -305,11 +378,12 @@ __global__ __launch_bounds__(256) void wino_weights_kernel(const float* w, int c
     }
 }
 
+// tile columns of a workgroup's block: 64, 32 or 16 (the kernel's instantiations), dividing the tile grid
 int wino_tc(int h, int w) {
     if (h % 2 || w % 4 || w < 32) return 0;
-    const int tc = w / 2 >= 64 ? 64 : w / 2;
-    if ((w / 2) % tc || (h / 2) % (WBT / tc)) return 0;
-    return tc;
+    for (int tc = 64; tc >= 16; tc /= 2)
+        if ((w / 2) % tc == 0 && (h / 2) % (WBT / tc) == 0) return tc;
+    return 0;
 }
 
 }  // namespace
@@ -360,8 +434,8 @@ SMC_API int smc_conv3x3_wino_f32(const float* x, int n, int cin, int h, int w, f
     const int64_t wgs = (int64_t)n * p.gx * p.gy * p.ntn;
     SMC_CHECK(wgs < (1LL << 31), "smc_conv3x3_wino_f32: grid too large");
     hipStream_t st = smc::as_stream(stream);
-    if (tc == 64) hipLaunchKernelGGL(wino_kernel<64>, dim3((unsigned)wgs), dim3(WNT), 0, st, p);
-    else if (tc == 32) hipLaunchKernelGGL(wino_kernel<32>, dim3((unsigned)wgs), dim3(WNT), 0, st, p);
-    else hipLaunchKernelGGL(wino_kernel<16>, dim3((unsigned)wgs), dim3(WNT), 0, st, p);
+    if (tc == 64) hipLaunchKernelGGL((wino_kernel<64, WOBW>), dim3((unsigned)wgs), dim3(64 * 8 / WOBW), 0, st, p);
+    else if (tc == 32) hipLaunchKernelGGL((wino_kernel<32, WOBW>), dim3((unsigned)wgs), dim3(64 * 8 / WOBW), 0, st, p);
+    else hipLaunchKernelGGL((wino_kernel<16, WOBW>), dim3((unsigned)wgs), dim3(64 * 8 / WOBW), 0, st, p);
     return smc::check_launch("smc_conv3x3_wino_f32");
 }

@@ -130,10 +130,10 @@ def wino_ok(n, cin, cout, h, w):
 
 def wino(x, y, uw, cin, cout, s=None, epi=None, alg_flops=0.0, alg_bytes=0):
     """One smc_conv3x3_wino_f32 launch (3x3, stride 1, pad 1).  alg_flops: the MFMA FLOPs it executes
-    (16 / 36 of the direct conv's)."""
+    (16 / 36 of the direct conv's; the timer also records the direct-equivalent count)."""
     n, _, h, w = x.shape
     tm = _hip.timer()
-    tok = tm.wrap(alg_flops, alg_bytes) if tm is not None else None
+    tok = tm.wrap(alg_flops, alg_bytes, kind="wino", equiv_flops=alg_flops * 36 / 16) if tm is not None else None
     _hip.call("smc_conv3x3_wino_f32", x.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(), _hip.ptr(s),
               ctypes.byref(epi) if epi is not None else None, _hip.stream())
     if tok is not None:

@@ -1,5 +1,5 @@
-"""HBM traffic per launch of the synthesis modconv GEMM family (conv_gemm_lds_kernel / conv_gemm_kernel /
-convt_gemm_kernel, TAG 0) from two rocprofv3 --pmc passes.
+"""HBM traffic per launch of the synthesis conv family (tools/conv_family.py: the direct implicit-GEMM kernels and
+the Winograd kernel, TAG 0) from two rocprofv3 --pmc passes.
 
     python tools/pmc_traffic.py FETCH.csv WRITE.csv > profiles/pmc_traffic.json
 
@@ -10,8 +10,12 @@ reads are 4-B buffer loads (uncalibrated width), so the figure is an estimate (t
 """
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from conv_family import is_family, is_wino  # noqa: E402
 
 
 def per_dispatch(path, counter):
@@ -29,16 +33,18 @@ def per_dispatch(path, counter):
 def main():
     fetch, names = per_dispatch(sys.argv[1], "FETCH_SIZE")
     write, names_w = per_dispatch(sys.argv[2], "WRITE_SIZE")
-    def fam(n):
-        return ("conv_gemm" in n or "convt_gemm_kernel" in n) and ", 1>(" not in n
+    def avg(vals, names, pred, scale):
+        sel = [v for d, v in vals.items() if pred(names[d])]
+        return scale * 1024 * sum(sel) / max(len(sel), 1), len(sel)
 
-    fam_r = [v for d, v in fetch.items() if fam(names[d])]
-    fam_w = [v for d, v in write.items() if fam(names_w[d])]
-    rd = 2 * 1024 * sum(fam_r) / max(len(fam_r), 1)
-    wr = 1024 * sum(fam_w) / max(len(fam_w), 1)
+    rd, nr = avg(fetch, names, is_family, 2)
+    wr, nw = avg(write, names_w, is_family, 1)
+    wrd, _ = avg(fetch, names, is_wino, 2)
+    wwr, nwino = avg(write, names_w, is_wino, 1)
     out = {"conv_gemm_bytes_per_launch": round(rd + wr),
            "read_bytes_per_launch": round(rd), "write_bytes_per_launch": round(wr),
-           "launches": [len(fam_r), len(fam_w)],
+           "launches": [nr, nw],
+           "wino_bytes_per_launch": round(wrd + wwr), "wino_launches": nwino,
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes over bench.py --steps 2 --warmup 1 "
                      "(+ its 2-step serialised roofline pass); "
                      "read = 2 x FETCH_SIZE KiB (gfx950 correction), write = WRITE_SIZE KiB"}

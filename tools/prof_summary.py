@@ -10,13 +10,15 @@ launches of the same kernels carry TAG 1 and are reported separately), whose ave
 bench.py's HIP-event roofline pass must match.
 """
 import csv
+import os
 import sys
 from collections import defaultdict
 
-FAMILY = ("conv_gemm_lds_kernel", "conv_gemm_kernel", "conv_row_kernel", "convt_gemm_kernel")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from conv_family import FAMILY, is_family as _is_family  # noqa: E402
 
 
-def is_family(name):
+def is_family(name):  # TAG 0 and TAG 1 (reported separately below)
     return any(f in name for f in FAMILY)
 
 

@@ -8,15 +8,18 @@ the GEMM kernel (TAG 0) plus, where the layer needs them, the per-sample weight 
 it (wscale_kernel) and the split-K reduction launched right after it (epilogue_kernel); the HIP events
 bracket all of them, so both the kernel-only and the whole-call averages are printed."""
 import csv
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from conv_family import is_family  # noqa: E402
 
 
 def main():
     path = sys.argv[1]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 100
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    is_fam = lambda r: ("conv_gemm" in r["Kernel_Name"] or "convt_gemm_kernel" in r["Kernel_Name"]) and \
-        ", 1>(" not in r["Kernel_Name"]
+    is_fam = lambda r: is_family(r["Kernel_Name"])
     idx = [i for i, r in enumerate(rows) if is_fam(r)][-n:]
     dur = lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     k_tot = sum(dur(rows[i]) for i in idx)
