@@ -64,49 +64,135 @@ struct GemmParams {
 };
 
 // Epilogue shared by the gather-GEMM kernels: lane owns column m, registers walk output channels.
+// The per-channel operands of the tile's BO channels (d[n, o] * scale_c[o] / scale_c[o], bias[o], alpha_c[o]) are
+// staged through LDS first (one global round trip per workgroup; `lds` must hold 3 * BO floats and is free once the
+// K loop is done), and the per-element ones (act_ref, residual) are gathered 16 at a time ahead of their stores:
+// loaded next to each store, every output channel would wait a global round trip behind the previous stores.
 template <int WO, int WM, int TO, int TM>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const PhaseDev& ph, const f32x16 (&acc)[TO][TM],
                                               int m0, int o0, int M, int hw_out, int split, int wo, int wm, int kh,
-                                              int l32) {
+                                              int l32, float* lds) {
+    constexpr int BO = WO * TO * 32;
+    constexpr int BM = WM * TM * 32;
+    const int64_t plane = (int64_t)p.y_h * p.y_w;
+    if (p.nsplit > 1) {  // raw partial sums of this split
+        float* dst = p.y + (int64_t)split * p.split_stride;
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+            const int mc = m0 + wm * TM * 32 + j * 32 + l32;
+            if (mc >= M) continue;
+            const int en = mc / hw_out;
+            const int erem = mc - en * hw_out;
+            const int ea = erem / ph.out_w;
+            const int64_t pix = (int64_t)(ph.out_oy + ph.out_sy * ea) * p.y_w + ph.out_ox + ph.out_sx * (erem - ea * ph.out_w);
+#pragma unroll
+            for (int i = 0; i < TO; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int o = o0 + wo * TO * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                    if (o < p.cout) dst[((int64_t)en * p.cout + o) * plane + pix] = acc[i][j][r];
+                }
+        }
+        return;
+    }
+    const int tid = threadIdx.x;
+    const int en0 = m0 / hw_out;
+    const bool one_img = (min(m0 + BM, M) - 1) / hw_out == en0;
+    const int mode = p.mode;
+    __syncthreads();  // every wave is done with the last K step's operand tiles
+    for (int t = tid; t < BO; t += NT) {
+        const int o = o0 + t;
+        float mul = 1.f, add = 0.f, al = 0.f;
+        if (o < p.cout) {
+            if (mode == SMC_EPI_MODACT) {
+                mul = (p.d && one_img ? p.d[(int64_t)en0 * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
+                add = p.bias ? p.bias[o] : 0.f;
+            } else if (mode == SMC_EPI_PRELU || mode == SMC_EPI_AFFINE) {
+                mul = p.ext.scale_c ? p.ext.scale_c[o] : 1.f;
+                add = p.bias ? p.bias[o] : 0.f;
+            }
+            if ((mode == SMC_EPI_PRELU || mode == SMC_EPI_PRELU_GRAD) && p.ext.alpha_c) al = p.ext.alpha_c[o];
+        }
+        lds[t] = mul;
+        lds[BO + t] = add;
+        lds[2 * BO + t] = al;
+    }
+    __syncthreads();
     const float nstr = p.noise_strength ? *p.noise_strength : 1.f;
-    float* dst = p.nsplit > 1 ? p.y + (int64_t)split * p.split_stride : p.y;
+    const int rs = p.ext.rs;
+    const int rh = p.y_h / rs, rw = p.y_w / rs;
+    // One straight-line body per epilogue mode (MODE is a compile-time constant inside it): with the mode tested per
+    // element every output would be its own branch region, and the loads of the next one would wait for the
+    // previous stores (vmcnt counts both).
+    auto body = [&](auto mode_c) {
+        constexpr int MODE = decltype(mode_c)::value;
+        constexpr bool EX_REF = MODE == SMC_EPI_PRELU_GRAD;  // per-element operand: act_ref (else the residual)
 #pragma unroll
-    for (int j = 0; j < TM; ++j) {
-        const int mc = m0 + wm * TM * 32 + j * 32 + l32;
-        if (mc >= M) continue;
-        const int en = mc / hw_out;
-        const int erem = mc - en * hw_out;
-        const int ea = erem / ph.out_w;
-        const int eb = erem - ea * ph.out_w;
-        const int yy = ph.out_oy + ph.out_sy * ea;
-        const int xx = ph.out_ox + ph.out_sx * eb;
-        const int64_t pix = (int64_t)yy * p.y_w + xx;
-        const int64_t plane = (int64_t)p.y_h * p.y_w;
-        float nz = 0.f;
-        if (p.nsplit == 1 && p.mode == SMC_EPI_MODACT && p.noise) nz = p.noise[en * p.noise_nstride + pix] * nstr;
+        for (int j = 0; j < TM; ++j) {
+            const int mc = m0 + wm * TM * 32 + j * 32 + l32;
+            if (mc >= M) continue;
+            const int en = mc / hw_out;
+            const int erem = mc - en * hw_out;
+            const int ea = erem / ph.out_w;
+            const int eb = erem - ea * ph.out_w;
+            const int yy = ph.out_oy + ph.out_sy * ea;
+            const int xx = ph.out_ox + ph.out_sx * eb;
+            const int64_t pix = (int64_t)yy * p.y_w + xx;
+            const bool res_here = p.ext.residual && yy % rs == 0 && xx % rs == 0;
+            const bool need_ex = EX_REF || p.ext.residual;
+            float nz = 0.f;
+            if (MODE == SMC_EPI_MODACT && p.noise) nz = p.noise[en * p.noise_nstride + pix] * nstr;
 #pragma unroll
-        for (int i = 0; i < TO; ++i) {
+            for (int i = 0; i < TO; ++i) {
+                const int ol0 = wo * TO * 32 + i * 32 + 4 * kh;  // tile-local channel of register r: ol0 + (r&3) + 8(r>>2)
+                float ex[16];
+                if (need_ex) {  // gathered before this row's stores
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int o = o0 + wo * TO * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-                if (o >= p.cout) continue;
-                const int64_t idx = ((int64_t)en * p.cout + o) * plane + pix;
-                const float v = acc[i][j][r];
-                if (p.nsplit > 1) {
-                    dst[idx] = v;
-                } else if (p.mode == SMC_EPI_MODACT) {
-                    if (p.u_save) p.u_save[idx] = v;
-                    const float dd = (p.d ? p.d[(int64_t)en * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
-                    float q = smc::epi_y(v, dd, nz, p.bias ? p.bias[o] : 0.f, p.act, p.alpha, p.gain, p.clamp);
-                    if (p.ext.residual) q = smc::epi_ext_apply(SMC_EPI_STORE, q, en, o, idx, yy, xx, p.cout, p.y_h, p.y_w,
-                                                                nullptr, nullptr, p.ext);
-                    dst[idx] = q;
-                } else {
-                    dst[idx] = smc::epi_ext_apply(p.mode, v, en, o, idx, yy, xx, p.cout, p.y_h, p.y_w, p.bias, p.u_save,
-                                                  p.ext);
+                    for (int r = 0; r < 16; ++r) {
+                        const int o = min(o0 + ol0 + (r & 3) + 8 * (r >> 2), p.cout - 1);
+                        if (EX_REF) ex[r] = p.ext.act_ref[((int64_t)en * p.cout + o) * plane + pix];
+                        else ex[r] = res_here ? p.ext.residual[(((int64_t)en * p.cout + o) * rh + yy / rs) * rw + xx / rs] : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int ol = ol0 + (r & 3) + 8 * (r >> 2);
+                    const int o = o0 + ol;
+                    if (o >= p.cout) continue;
+                    const int64_t idx = ((int64_t)en * p.cout + o) * plane + pix;
+                    const float v = acc[i][j][r];
+                    float q;
+                    if constexpr (MODE == SMC_EPI_MODACT) {
+                        if (p.u_save) p.u_save[idx] = v;
+                        const float dd = one_img ? lds[ol]
+                                                 : (p.d ? p.d[(int64_t)en * p.cout + o] : 1.f) *
+                                                       (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
+                        q = smc::epi_y(v, dd, nz, lds[BO + ol], p.act, p.alpha, p.gain, p.clamp);
+                    } else if constexpr (MODE == SMC_EPI_PRELU) {
+                        const float z = v * lds[ol] + lds[BO + ol];
+                        if (p.u_save) p.u_save[idx] = z;
+                        q = z >= 0.f ? z : z * lds[2 * BO + ol];
+                    } else if constexpr (MODE == SMC_EPI_PRELU_GRAD) {
+                        q = ex[r] >= 0.f ? v : v * lds[2 * BO + ol];
+                        if (res_here)  // (no caller combines the two)
+                            q += p.ext.residual[(((int64_t)en * p.cout + o) * rh + yy / rs) * rw + xx / rs];
+                    } else if constexpr (MODE == SMC_EPI_AFFINE) {
+                        q = v * lds[ol] + lds[BO + ol];
+                    } else {
+                        q = v;
+                    }
+                    if (!EX_REF && need_ex) q += ex[r];  // the residual (0 off its stride grid)
+                    p.y[idx] = q;
                 }
             }
         }
+    };
+    switch (mode) {
+        case SMC_EPI_MODACT: body(std::integral_constant<int, SMC_EPI_MODACT>{}); break;
+        case SMC_EPI_PRELU: body(std::integral_constant<int, SMC_EPI_PRELU>{}); break;
+        case SMC_EPI_PRELU_GRAD: body(std::integral_constant<int, SMC_EPI_PRELU_GRAD>{}); break;
+        case SMC_EPI_AFFINE: body(std::integral_constant<int, SMC_EPI_AFFINE>{}); break;
+        default: body(std::integral_constant<int, SMC_EPI_STORE>{}); break;
     }
 }
 
@@ -288,7 +374,7 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(GemmParams p) {
         stage ^= 1;
     }
 
-    gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32);
+    gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32, smem);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -486,7 +572,7 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_lds_kernel(GemmParams p) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragment reads of this slot done before the next barrier
     }
-    gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32);
+    gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32, smem);
 }
 
 // Row-halo variant for the 3x3 stride-1 'same' convs whose position tiles are row segments (W % BM == 0: the
@@ -627,7 +713,7 @@ __global__ __launch_bounds__(NT, 2) void conv_row_kernel(GemmParams p, RowTaps r
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, p.n * hw, hw, 0, wo, wm, kh, l32);
+    gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, p.n * hw, hw, 0, wo, wm, kh, l32, smem);
 }
 
 // Style-scaled input for the low-resolution layers: out[n][i][p] = x[n][i][p] * s[n][i] (float4 when hw % 4 == 0).

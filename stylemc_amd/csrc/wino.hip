@@ -160,6 +160,28 @@ void wino_kernel(WinoParams p) {
     const int tr = tl / TC, tc = tl - tr * TC;
     const int poff = kq_lane * SLAB + 2 * tr * PITCH + 2 * tc + 3;
     const int uoff = (kq_lane * 4 * WBO + 16 * ob16 + (lane & 15)) * 4;
+    const int yy0 = 2 * (ty0 + tr), xx0 = 2 * (tx0 + tc);
+    // The MODACT epilogue's per-channel / per-pixel operands, loaded before the K loop: issued after the epilogue's
+    // first stores (which may alias them) they would cost one global round trip per output channel.
+    float e_d[OBW][4], e_b[OBW][4], nz[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    if (p.mode == SMC_EPI_MODACT) {
+#pragma unroll
+        for (int b = 0; b < OBW; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = o0 + 16 * (ob16 + b) + 4 * kq_lane + r;
+                e_d[b][r] = (p.d ? p.d[(int64_t)nn * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
+                e_b[b][r] = p.bias ? p.bias[o] : 0.f;
+            }
+        if (p.noise) {
+            const float nstr = p.noise_strength ? *p.noise_strength : 1.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    nz[i][j] = p.noise[nn * p.noise_nstride + (int64_t)(yy0 + i) * W + xx0 + j] * nstr;
+        }
+    }
     const bool has_s = p.s != nullptr;
     const float* srow = has_s ? p.s + (int64_t)nn * p.cin + kq_lane : p.x;
     float sv[2] = {1.f, 1.f}, sn[2] = {1.f, 1.f};
@@ -281,15 +303,6 @@ void wino_kernel(WinoParams p) {
         if (sum == 12345.f) p.y[tid] = sum;
         return;
     }
-    const int yy0 = 2 * (ty0 + tr), xx0 = 2 * (tx0 + tc);
-    const float nstr = p.noise_strength ? *p.noise_strength : 1.f;
-    float nz[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-    if (p.mode == SMC_EPI_MODACT && p.noise) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) nz[i][j] = p.noise[nn * p.noise_nstride + (int64_t)(yy0 + i) * W + xx0 + j] * nstr;
-    }
 #pragma unroll
     for (int b = 0; b < OBW; ++b) {
 #pragma unroll
@@ -312,8 +325,7 @@ void wino_kernel(WinoParams p) {
             }
             const int64_t obase = ((int64_t)nn * p.cout + o) * plane;
             if (p.mode == SMC_EPI_MODACT) {
-                const float dsc = (p.d ? p.d[(int64_t)nn * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
-                const float bo = p.bias ? p.bias[o] : 0.f;
+                const float dsc = e_d[b][r], bo = e_b[b][r];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     const int64_t idx = obase + (int64_t)(yy0 + i) * W + xx0;
