@@ -61,6 +61,40 @@ def generate_image(G, until_k, styles, temp_shapes, noise_mode="const", device=N
     return xs, img
 
 
+_GATHER_IDX = {}
+
+
+def _gather_rows(G, until_k, styles, temp_shapes, full=()):
+    """Every S row a layer of the synthesis reads, cut to the layer's width, as contiguous [N, width] tensors from
+    ONE gather (index_select) -- the per-layer views styles[:, r, :width] would each cost a copy kernel (the layers
+    take contiguous style rows).  {row: tensor}; rows in `full` keep all columns (the trainable rows: delta is added
+    before the cut); rows past until_k are not gathered."""
+    n = styles.shape[0]
+    specs = []
+    row = 0
+    for k, res in enumerate(G.synthesis.block_resolutions):
+        width = 2 if res == 4 else 3
+        if k <= until_k:
+            sh = temp_shapes[k]
+            widths = (sh[0], sh[2]) if res == 4 else tuple(sh)
+            specs += [(row + j, styles.shape[2] if row + j in full else widths[j]) for j in range(width)]
+        row += width
+    styles = styles.contiguous()
+    key = (n, styles.shape[1], styles.shape[2], tuple(specs), styles.device)
+    idx = _GATHER_IDX.get(key)
+    if idx is None:
+        nr, c = styles.shape[1], styles.shape[2]
+        base = torch.arange(n).view(n, 1) * (nr * c)
+        idx = torch.cat([(base + r * c + torch.arange(w).view(1, w)).reshape(-1) for r, w in specs]).to(styles.device)
+        _GATHER_IDX[key] = idx
+    flat = styles.reshape(-1).index_select(0, idx)
+    out, off = {}, 0
+    for r, w in specs:
+        out[r] = flat[off:off + n * w].view(n, w)
+        off += n * w
+    return out
+
+
 def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", delta=None,
                         trainable=S_TRAINABLE_SPACE_CHANNELS):
     """generate_image(G, until_k, styles + direction) where the direction lives only on `trainable` rows.
@@ -72,6 +106,7 @@ def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", del
     """
     x = img = None
     row = 0
+    gathered = _gather_rows(G, until_k, styles, temp_shapes, full=set(trainable) if delta is not None else ())
     for k, res in enumerate(G.synthesis.block_resolutions):
         if k > until_k:
             continue
@@ -80,7 +115,7 @@ def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", del
         rows = []
         for j in range(width):
             r = row + j
-            w = styles[:, r]
+            w = gathered[r]
             if delta is not None and r in trainable:
                 w = w + delta[:, trainable.index(r)]
             rows.append(w)
