@@ -54,3 +54,20 @@ def test_cpu_tensors_rejected():
         bias_act.bias_act(x, act="lrelu")
     with pytest.raises(RuntimeError):
         upfirdn2d.upsample2d(x, upfirdn2d.setup_filter([1, 3, 3, 1]))
+
+
+def test_wino_shape_support_without_gpu():
+    """smc_conv3x3_wino_supported is host logic (no device call): every synthesis conv1 from 32 px up has a
+    Winograd kernel; narrower, odd-width, non-multiple-of-8 / 32 channel and >= 2 GiB inputs do not."""
+    lib = _hip.load()
+    for r in (32, 64, 128, 256, 512, 1024):
+        c = min(32768 // r, 512)
+        assert lib.smc_conv3x3_wino_supported(4, c, c, r, r) == 1, r
+    assert lib.smc_conv3x3_wino_supported(4, 512, 512, 16, 16) == 0      # w < 32
+    assert lib.smc_conv3x3_wino_supported(1, 64, 64, 112, 112) == 0     # 56 tile columns: no 64/32/16 block divides
+    assert lib.smc_conv3x3_wino_supported(1, 64, 64, 96, 96) == 1       # 48 tile columns -> 16-column blocks
+    assert lib.smc_conv3x3_wino_supported(1, 64, 64, 66, 64) == 0       # 33 tile rows: no 4-row block divides
+    assert lib.smc_conv3x3_wino_supported(1, 64, 64, 64, 34) == 0       # w % 4
+    assert lib.smc_conv3x3_wino_supported(1, 12, 32, 64, 64) == 0       # cin % 8
+    assert lib.smc_conv3x3_wino_supported(1, 32, 48, 64, 64) == 0       # cout % 32
+    assert lib.smc_conv3x3_wino_supported(16, 512, 512, 256, 256) == 0  # input >= 2 GiB (32-bit buffer offsets)
