@@ -25,6 +25,7 @@
 //     LDS, transforms it in registers (32 adds; x s[n, c] for the style-scaled forward) and that is its B
 //     fragment for all 16 xi -- V never goes through LDS.  A fragments: 8 ds_read_b128 (bank-conflict free).
 #include <algorithm>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -303,57 +304,78 @@ void wino_kernel(WinoParams p) {
         if (sum == 12345.f) p.y[tid] = sum;
         return;
     }
+    // The synthesis' two MODACT forms get a body with the activation fixed at compile time (KIND 1: lrelu with
+    // 0 <= alpha <= 1, gain, clamp -- the conv1 forward; KIND 2: linear, no clamp -- the data gradient's x s[n, i]):
+    // lrelu(z) = max(z, alpha z) and clamp = min / max, bit-identical to smc::epi_y for every finite value, without
+    // the per-element tests of the runtime activation.  KIND 0: any epilogue through smc::epi_y / epi_ext_apply.
+    auto body = [&](auto kind_c) {
+        constexpr int KIND = decltype(kind_c)::value;
 #pragma unroll
-    for (int b = 0; b < OBW; ++b) {
+        for (int b = 0; b < OBW; ++b) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int o = o0 + 16 * (ob16 + b) + 4 * kq_lane + r;
-            float m[4][4];
+            for (int r = 0; r < 4; ++r) {
+                const int o = o0 + 16 * (ob16 + b) + 4 * kq_lane + r;
+                float m[4][4];
 #pragma unroll
-            for (int xi = 0; xi < 16; ++xi) m[xi >> 2][xi & 3] = acc[xi][b][r];
-            float rr[2][4];
+                for (int xi = 0; xi < 16; ++xi) m[xi >> 2][xi & 3] = acc[xi][b][r];
+                float rr[2][4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                rr[0][j] = m[0][j] + m[1][j] + m[2][j];
-                rr[1][j] = m[1][j] - m[2][j] - m[3][j];
-            }
-            float out[2][2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                out[i][0] = rr[i][0] + rr[i][1] + rr[i][2];
-                out[i][1] = rr[i][1] - rr[i][2] - rr[i][3];
-            }
-            const int64_t obase = ((int64_t)nn * p.cout + o) * plane;
-            if (p.mode == SMC_EPI_MODACT) {
-                const float dsc = e_d[b][r], bo = e_b[b][r];
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const int64_t idx = obase + (int64_t)(yy0 + i) * W + xx0;
-                    if (p.u_save) *reinterpret_cast<float2*>(p.u_save + idx) = make_float2(out[i][0], out[i][1]);
-                    float q[2];
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        q[j] = smc::epi_y(out[i][j], dsc, nz[i][j], bo, p.act, p.alpha, p.gain, p.clamp);
-                        if (p.ext.residual)
-                            q[j] = smc::epi_ext_apply(SMC_EPI_STORE, q[j], nn, o, idx + j, yy0 + i, xx0 + j, p.cout, H, W,
-                                                      nullptr, nullptr, p.ext);
-                    }
-                    *reinterpret_cast<float2*>(p.y + idx) = make_float2(q[0], q[1]);
+                for (int j = 0; j < 4; ++j) {
+                    rr[0][j] = m[0][j] + m[1][j] + m[2][j];
+                    rr[1][j] = m[1][j] - m[2][j] - m[3][j];
                 }
-            } else {
+                float out[2][2];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    const int64_t idx = obase + (int64_t)(yy0 + i) * W + xx0;
-                    float q[2];
+                    out[i][0] = rr[i][0] + rr[i][1] + rr[i][2];
+                    out[i][1] = rr[i][1] - rr[i][2] - rr[i][3];
+                }
+                const int64_t obase = ((int64_t)nn * p.cout + o) * plane;
+                if (KIND != 0 || p.mode == SMC_EPI_MODACT) {
+                    const float dsc = e_d[b][r], bo = e_b[b][r];
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        q[j] = smc::epi_ext_apply(p.mode, out[i][j], nn, o, idx + j, yy0 + i, xx0 + j, p.cout, H, W, p.bias,
-                                                  p.u_save, p.ext);
-                    *reinterpret_cast<float2*>(p.y + idx) = make_float2(q[0], q[1]);
+                    for (int i = 0; i < 2; ++i) {
+                        const int64_t idx = obase + (int64_t)(yy0 + i) * W + xx0;
+                        if (p.u_save) *reinterpret_cast<float2*>(p.u_save + idx) = make_float2(out[i][0], out[i][1]);
+                        float q[2];
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            if constexpr (KIND == 1) {
+                                const float z = __fmaf_rn(out[i][j], dsc, nz[i][j]) + bo;
+                                q[j] = fmaxf(fminf(fmaxf(z, z * p.alpha) * p.gain, p.clamp), -p.clamp);
+                            } else if constexpr (KIND == 2) {
+                                q[j] = (__fmaf_rn(out[i][j], dsc, nz[i][j]) + bo) * p.gain;
+                            } else {
+                                q[j] = smc::epi_y(out[i][j], dsc, nz[i][j], bo, p.act, p.alpha, p.gain, p.clamp);
+                                if (p.ext.residual)
+                                    q[j] = smc::epi_ext_apply(SMC_EPI_STORE, q[j], nn, o, idx + j, yy0 + i, xx0 + j, p.cout,
+                                                              H, W, nullptr, nullptr, p.ext);
+                            }
+                        }
+                        *reinterpret_cast<float2*>(p.y + idx) = make_float2(q[0], q[1]);
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const int64_t idx = obase + (int64_t)(yy0 + i) * W + xx0;
+                        float q[2];
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            q[j] = smc::epi_ext_apply(p.mode, out[i][j], nn, o, idx + j, yy0 + i, xx0 + j, p.cout, H, W,
+                                                      p.bias, p.u_save, p.ext);
+                        *reinterpret_cast<float2*>(p.y + idx) = make_float2(q[0], q[1]);
+                    }
                 }
             }
         }
-    }
+    };
+    const bool modact_plain = p.mode == SMC_EPI_MODACT && !p.ext.residual;
+    if (modact_plain && p.act == SMC_ACT_LRELU && p.alpha >= 0.f && p.alpha <= 1.f && p.clamp >= 0.f)
+        body(std::integral_constant<int, 1>{});
+    else if (modact_plain && p.act == SMC_ACT_LINEAR && p.clamp < 0.f)
+        body(std::integral_constant<int, 2>{});
+    else
+        body(std::integral_constant<int, 0>{});
 }
 
 // U = G g G^T per (k, n): flip = 0: g = w[n][k] (k = cin, n = cout: the forward correlation);
