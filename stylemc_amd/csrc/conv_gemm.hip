@@ -124,8 +124,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const PhaseDe
     // One straight-line body per epilogue mode (MODE is a compile-time constant inside it): with the mode tested per
     // element every output would be its own branch region, and the loads of the next one would wait for the
     // previous stores (vmcnt counts both).
-    auto body = [&](auto mode_c) {
+    auto body = [&](auto mode_c, auto kind_c) {
         constexpr int MODE = decltype(mode_c)::value;
+        constexpr int KIND = decltype(kind_c)::value;  // MODACT: 1 lrelu (0 <= alpha <= 1) + clamp, 2 linear, 0 any
         constexpr bool EX_REF = MODE == SMC_EPI_PRELU_GRAD;  // per-element operand: act_ref (else the residual)
 #pragma unroll
         for (int j = 0; j < TM; ++j) {
@@ -167,7 +168,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const PhaseDe
                         const float dd = one_img ? lds[ol]
                                                  : (p.d ? p.d[(int64_t)en * p.cout + o] : 1.f) *
                                                        (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
-                        q = smc::epi_y(v, dd, nz, lds[BO + ol], p.act, p.alpha, p.gain, p.clamp);
+                        if constexpr (KIND == 1) {  // max / min forms: bit-identical to epi_y for finite values
+                            const float z = __fmaf_rn(v, dd, nz) + lds[BO + ol];
+                            q = fmaxf(fminf(fmaxf(z, z * p.alpha) * p.gain, p.clamp), -p.clamp);
+                        } else if constexpr (KIND == 2) {
+                            q = (__fmaf_rn(v, dd, nz) + lds[BO + ol]) * p.gain;
+                        } else {
+                            q = smc::epi_y(v, dd, nz, lds[BO + ol], p.act, p.alpha, p.gain, p.clamp);
+                        }
                     } else if constexpr (MODE == SMC_EPI_PRELU) {
                         const float z = v * lds[ol] + lds[BO + ol];
                         if (p.u_save) p.u_save[idx] = z;
@@ -187,12 +195,20 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const PhaseDe
             }
         }
     };
+    using K0 = std::integral_constant<int, 0>;
     switch (mode) {
-        case SMC_EPI_MODACT: body(std::integral_constant<int, SMC_EPI_MODACT>{}); break;
-        case SMC_EPI_PRELU: body(std::integral_constant<int, SMC_EPI_PRELU>{}); break;
-        case SMC_EPI_PRELU_GRAD: body(std::integral_constant<int, SMC_EPI_PRELU_GRAD>{}); break;
-        case SMC_EPI_AFFINE: body(std::integral_constant<int, SMC_EPI_AFFINE>{}); break;
-        default: body(std::integral_constant<int, SMC_EPI_STORE>{}); break;
+        case SMC_EPI_MODACT:
+            if (p.act == SMC_ACT_LRELU && p.alpha >= 0.f && p.alpha <= 1.f && p.clamp >= 0.f)
+                body(std::integral_constant<int, SMC_EPI_MODACT>{}, std::integral_constant<int, 1>{});
+            else if (p.act == SMC_ACT_LINEAR && p.clamp < 0.f)
+                body(std::integral_constant<int, SMC_EPI_MODACT>{}, std::integral_constant<int, 2>{});
+            else
+                body(std::integral_constant<int, SMC_EPI_MODACT>{}, K0{});
+            break;
+        case SMC_EPI_PRELU: body(std::integral_constant<int, SMC_EPI_PRELU>{}, K0{}); break;
+        case SMC_EPI_PRELU_GRAD: body(std::integral_constant<int, SMC_EPI_PRELU_GRAD>{}, K0{}); break;
+        case SMC_EPI_AFFINE: body(std::integral_constant<int, SMC_EPI_AFFINE>{}, K0{}); break;
+        default: body(std::integral_constant<int, SMC_EPI_STORE>{}, K0{}); break;
     }
 }
 

@@ -386,6 +386,22 @@ __global__ __launch_bounds__(256) void blur_act_v4(const float* t, int nsplit, i
     const int64_t plane = nc * (int64_t)y_h * y_w;
     const int ox = ox0 + 2 * tx;
     if (ox >= y_w) return;
+    // the 4 rows' noise is loaded before the first store (loaded next to each store, every row would wait for the
+    // previous row's stores: vmcnt counts both)
+    float2 nz[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int oy = min(oy0 + 4 * ty + i, y_h - 1);
+        nz[i] = make_float2(0.f, 0.f);
+        if (e.mode != SMC_EPI_STORE && e.noise) {
+            nz[i] = *reinterpret_cast<const float2*>(e.noise + n * e.noise_nstride + (int64_t)oy * y_w + ox);
+            nz[i].x *= nstr;
+            nz[i].y *= nstr;
+        }
+    }
+    // the synthesis' conv0 epilogue (lrelu with 0 <= alpha <= 1, gain, clamp >= 0) with the activation fixed at
+    // compile time: max / min forms, bit-identical to smc::epi_y for finite values
+    const bool lrelu_clamp = e.act == SMC_ACT_LRELU && e.alpha >= 0.f && e.alpha <= 1.f && e.clamp >= 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int oy = oy0 + 4 * ty + i;
@@ -397,15 +413,16 @@ __global__ __launch_bounds__(256) void blur_act_v4(const float* t, int nsplit, i
             continue;
         }
         if (e.u_save) *reinterpret_cast<float2*>(e.u_save + plane + pix) = u2;
-        float2 nz = make_float2(0.f, 0.f);
-        if (e.noise) {
-            nz = *reinterpret_cast<const float2*>(e.noise + n * e.noise_nstride + pix);
-            nz.x *= nstr;
-            nz.y *= nstr;
+        float2 q;
+        if (lrelu_clamp) {
+            const float zx = __fmaf_rn(u2.x, dv, nz[i].x) + bv, zy = __fmaf_rn(u2.y, dv, nz[i].y) + bv;
+            q.x = fmaxf(fminf(fmaxf(zx, zx * e.alpha) * e.gain, e.clamp), -e.clamp);
+            q.y = fmaxf(fminf(fmaxf(zy, zy * e.alpha) * e.gain, e.clamp), -e.clamp);
+        } else {
+            q = make_float2(smc::epi_y(u2.x, dv, nz[i].x, bv, e.act, e.alpha, e.gain, e.clamp),
+                            smc::epi_y(u2.y, dv, nz[i].y, bv, e.act, e.alpha, e.gain, e.clamp));
         }
-        *reinterpret_cast<float2*>(y + plane + pix) =
-            make_float2(smc::epi_y(u2.x, dv, nz.x, bv, e.act, e.alpha, e.gain, e.clamp),
-                        smc::epi_y(u2.y, dv, nz.y, bv, e.act, e.alpha, e.gain, e.clamp));
+        *reinterpret_cast<float2*>(y + plane + pix) = q;
     }
 }
 
