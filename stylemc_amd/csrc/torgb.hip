@@ -174,33 +174,48 @@ __global__ __launch_bounds__(256) void torgb_act_bwd_kernel(const float* g_rgb, 
         }
     }
     const int64_t base = (int64_t)nn * cin * hw + p0;
-    for (int k = 0; k < cin; ++k) {
-        const int64_t off = base + (int64_t)k * hw;
-        float gn[V], yk[V], r[V];
-        if (VEC) {
-            const float4 a = g_next ? *reinterpret_cast<const float4*>(g_next + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 b = *reinterpret_cast<const float4*>(y + off);
-            gn[0] = a.x; gn[V > 1 ? 1 : 0] = a.y; gn[V > 2 ? 2 : 0] = a.z; gn[V > 3 ? 3 : 0] = a.w;
-            yk[0] = b.x; yk[V > 1 ? 1 : 0] = b.y; yk[V > 2 ? 2 : 0] = b.z; yk[V > 3 ? 3 : 0] = b.w;
-        } else {
-            gn[0] = g_next ? g_next[off] : 0.f;
-            yk[0] = y[off];
-        }
-        const float dk = d ? d[(int64_t)nn * cin + k] : 1.f;
+    // Channels in chunks of KC: every load of a chunk is issued before its stores (one at a time, each channel's
+    // loads would wait for the previous channel's store: vmcnt counts both).
+    constexpr int KC = 8;
+    for (int k0 = 0; k0 < cin; k0 += KC) {
+        float gn[KC][V], yk[KC][V], dkv[KC];
 #pragma unroll
-        for (int v = 0; v < V; ++v) {
-            float t = 0.f;
-#pragma unroll
-            for (int c = 0; c < kMaxOut; ++c) {
-                if (c >= cout) break;
-                t += ws[c * cin + k] * gm[c][v];
+        for (int kk = 0; kk < KC; ++kk) {
+            const int k = min(k0 + kk, cin - 1);
+            const int64_t off = base + (int64_t)k * hw;
+            dkv[kk] = d ? d[(int64_t)nn * cin + k] : 1.f;
+            if (VEC) {
+                const float4 a = g_next ? *reinterpret_cast<const float4*>(g_next + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 b = *reinterpret_cast<const float4*>(y + off);
+                gn[kk][0] = a.x; gn[kk][V > 1 ? 1 : 0] = a.y; gn[kk][V > 2 ? 2 : 0] = a.z; gn[kk][V > 3 ? 3 : 0] = a.w;
+                yk[kk][0] = b.x; yk[kk][V > 1 ? 1 : 0] = b.y; yk[kk][V > 2 ? 2 : 0] = b.z; yk[kk][V > 3 ? 3 : 0] = b.w;
+            } else {
+                gn[kk][0] = g_next ? g_next[off] : 0.f;
+                yk[kk][0] = y[off];
             }
-            const float gy = g_next ? gn[v] + t : t;
-            r[v] = smc::act_grad_y(act, gy, yk[v], alpha, gain, clamp) * dk;
         }
-        if (VEC) *reinterpret_cast<float4*>(du + off) = make_float4(r[0], r[V > 1 ? 1 : 0], r[V > 2 ? 2 : 0],
-                                                                    r[V > 3 ? 3 : 0]);
-        else du[off] = r[0];
+#pragma unroll
+        for (int kk = 0; kk < KC; ++kk) {
+            const int k = k0 + kk;
+            if (k >= cin) break;
+            const int64_t off = base + (int64_t)k * hw;
+            const float dk = dkv[kk];
+            float r[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                float t = 0.f;
+#pragma unroll
+                for (int c = 0; c < kMaxOut; ++c) {
+                    if (c >= cout) break;
+                    t += ws[c * cin + k] * gm[c][v];
+                }
+                const float gy = g_next ? gn[kk][v] + t : t;
+                r[v] = smc::act_grad_y(act, gy, yk[kk][v], alpha, gain, clamp) * dk;
+            }
+            if (VEC) *reinterpret_cast<float4*>(du + off) = make_float4(r[0], r[V > 1 ? 1 : 0], r[V > 2 ? 2 : 0],
+                                                                        r[V > 3 ? 3 : 0]);
+            else du[off] = r[0];
+        }
     }
 }
 
