@@ -65,8 +65,16 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const float* src, int nsp
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t hw = (int64_t)h * w;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
+        // partials 8 at a time, all loads in flight before the adds (in split order, as one at a time)
         float v = src[idx];
-        for (int s = 1; s < nsplit; ++s) v += src[s * split_stride + idx];
+        for (int s0 = 1; s0 < nsplit; s0 += 8) {
+            float t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t[k] = src[min(s0 + k, nsplit - 1) * split_stride + idx];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (s0 + k < nsplit) v += t[k];
+        }
         if (e.mode == SMC_EPI_STORE && !e.ext.residual) {
             y[idx] = v;
             continue;

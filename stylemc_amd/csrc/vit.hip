@@ -482,11 +482,15 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* x, int64_t ldx
     if (row >= M) return;
     const int nv = D >> 6;
     const float* xr = x + row * ldx;
+    // every load issued before the first add (clamped column, zeroed past the row): loaded under a `t < nv`
+    // branch, each add waited out its own load
     float v[LN_MAXV];
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) v[t] = xr[lane + 64 * min(t, nv - 1)];
     float s = 0.f;
 #pragma unroll
     for (int t = 0; t < LN_MAXV; ++t) {
-        v[t] = t < nv ? xr[lane + 64 * t] : 0.f;
+        v[t] = t < nv ? v[t] : 0.f;
         s += v[t];
     }
     const float mean = wave_sum(s) / D;
@@ -519,17 +523,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* dy, int64_t ld
     const int nv = D >> 6;
     const float mean = mean_in[row], rstd = rstd_in[row];
     float g[LN_MAXV], xh[LN_MAXV];
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) {  // all loads first (clamped column), as in ln_fwd_kernel
+        const int c = lane + 64 * min(t, nv - 1);
+        g[t] = dy[row * lddy + c] * w[c];
+        xh[t] = (x[row * ldx + c] - mean) * rstd;
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int t = 0; t < LN_MAXV; ++t) {
-        if (t < nv) {
-            const int c = lane + 64 * t;
-            g[t] = dy[row * lddy + c] * w[c];
-            xh[t] = (x[row * ldx + c] - mean) * rstd;
-        } else {
-            g[t] = 0.f;
-            xh[t] = 0.f;
-        }
+        g[t] = t < nv ? g[t] : 0.f;
+        xh[t] = t < nv ? xh[t] : 0.f;
         s1 += g[t];
         s2 += g[t] * xh[t];
     }
