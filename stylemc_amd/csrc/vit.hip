@@ -557,6 +557,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* dy, int64_t ld
 
 constexpr int HD = 64, HP = 65, AQB = 16, AQB_BWD_SINGLE = 64;
 
+// Stage `rows` rows of 64 floats (global row stride ld) into LDS rows of pitch HP, times `mul`; rows >= valid
+// are zero.  Eight elements per thread are loaded before any is written: written as they arrive, every LDS
+// store waited out its own global round trip (the staging was most of the attention kernels' time).
+__device__ __forceinline__ void stage_rows64(float* dst, const float* src, int64_t ld, int rows, int valid, float mul) {
+    constexpr int CH = 8;
+    const int n = rows * HD;
+    for (int i0 = threadIdx.x; i0 < n; i0 += 256 * CH) {
+        float v[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int idx = i0 + 256 * k;
+            v[k] = src[(int64_t)min(idx >> 6, valid - 1) * ld + (idx & 63)];
+        }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int idx = i0 + 256 * k, j = idx >> 6;
+            if (idx < n) dst[j * HP + (idx & 63)] = j < valid ? v[k] * mul : 0.f;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* qkv, float* out, float* psave, int L, int H,
                                                        float scale, int causal) {
     extern __shared__ float sm[];
@@ -568,17 +589,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* qkv, float* 
     const int q0 = blockIdx.x * AQB, h = blockIdx.y, b = blockIdx.z;
     const int D = H * HD, ld = 3 * D;
     const float* base = qkv + (int64_t)b * L * ld + h * HD;
-    for (int idx = tid; idx < L * HD; idx += 256) {
-        const int j = idx >> 6, d = idx & 63;
-        Ks[j * HP + d] = base[(int64_t)j * ld + D + d];
-        Vs[j * HP + d] = base[(int64_t)j * ld + 2 * D + d];
-    }
-    for (int idx = tid; idx < AQB * HD; idx += 256) {
-        const int i = idx >> 6, d = idx & 63;
-        Qs[i * HP + d] = q0 + i < L ? base[(int64_t)(q0 + i) * ld + d] * scale : 0.f;
-    }
-    __syncthreads();
     const int nq = min(AQB, L - q0);
+    stage_rows64(Ks, base + D, ld, L, L, 1.f);
+    stage_rows64(Vs, base + 2 * D, ld, L, L, 1.f);
+    stage_rows64(Qs, base + (int64_t)q0 * ld, ld, AQB, nq, scale);
+    __syncthreads();
     for (int idx = tid; idx < nq * L; idx += 256) {
         const int i = idx / L, j = idx - i * L;
         float s = 0.f;
@@ -632,19 +647,21 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float* dout, const 
     const int D = H * HD, ld = 3 * D;
     const int nq = min(QB, L - q0);
     const float* base = qkv + (int64_t)b * L * ld + h * HD;
-    for (int idx = tid; idx < L * HD; idx += 256) {
-        const int j = idx >> 6, d = idx & 63;
-        Ks[j * HP + d] = base[(int64_t)j * ld + D + d];
-        Vs[j * HP + d] = base[(int64_t)j * ld + 2 * D + d];
-    }
-    for (int idx = tid; idx < QB * HD; idx += 256) {
-        const int i = idx >> 6, d = idx & 63;
-        const bool ok = i < nq;
-        Qs[i * HP + d] = ok ? base[(int64_t)(q0 + i) * ld + d] * scale : 0.f;
-        dOs[i * HP + d] = ok ? dout[((int64_t)b * L + q0 + i) * D + h * HD + d] : 0.f;
-    }
+    stage_rows64(Ks, base + D, ld, L, L, 1.f);
+    stage_rows64(Vs, base + 2 * D, ld, L, L, 1.f);
+    stage_rows64(Qs, base + (int64_t)q0 * ld, ld, QB, nq, scale);
+    stage_rows64(dOs, dout + ((int64_t)b * L + q0) * D + h * HD, D, QB, nq, 1.f);
     const float* pbase = psave + (((int64_t)b * H + h) * L + q0) * L;
-    for (int idx = tid; idx < QB * L; idx += 256) Ps[idx] = idx < nq * L ? pbase[idx] : 0.f;
+    for (int i0 = tid; i0 < QB * L; i0 += 256 * 8) {  // P block: loads first, as in stage_rows64
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = pbase[min(i0 + 256 * k, nq * L - 1)];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int idx = i0 + 256 * k;
+            if (idx < QB * L) Ps[idx] = idx < nq * L ? v[k] : 0.f;
+        }
+    }
     __syncthreads();
     for (int idx = tid; idx < nq * L; idx += 256) {
         const int i = idx / L, j = idx - i * L;
