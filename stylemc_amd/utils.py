@@ -64,11 +64,12 @@ def generate_image(G, until_k, styles, temp_shapes, noise_mode="const", device=N
 _GATHER_IDX = {}
 
 
-def _gather_rows(G, until_k, styles, temp_shapes, full=()):
+def _gather_rows(G, until_k, styles, temp_shapes, full=(), lead=()):
     """Every S row a layer of the synthesis reads, cut to the layer's width, as contiguous [N, width] tensors from
     ONE gather (index_select) -- the per-layer views styles[:, r, :width] would each cost a copy kernel (the layers
-    take contiguous style rows).  {row: tensor}; rows in `full` keep all columns (the trainable rows: delta is added
-    before the cut); rows past until_k are not gathered."""
+    take contiguous style rows).  Returns ({row: tensor}, block): rows in `full` keep all columns (the trainable
+    rows: delta is added before the cut); rows past until_k are not gathered.  The rows of `lead` (all of them
+    gathered, in `full`) come first, in that order, and `block` is them as one [len(lead), N, C] tensor (else None)."""
     n = styles.shape[0]
     specs = []
     row = 0
@@ -79,6 +80,9 @@ def _gather_rows(G, until_k, styles, temp_shapes, full=()):
             widths = (sh[0], sh[2]) if res == 4 else tuple(sh)
             specs += [(row + j, styles.shape[2] if row + j in full else widths[j]) for j in range(width)]
         row += width
+    rows = {r for r, _ in specs}
+    lead = tuple(lead) if lead and all(r in rows and r in full for r in lead) else ()
+    specs = [sp for r in lead for sp in specs if sp[0] == r] + [sp for sp in specs if sp[0] not in lead]
     styles = styles.contiguous()
     key = (n, styles.shape[1], styles.shape[2], tuple(specs), styles.device)
     idx = _GATHER_IDX.get(key)
@@ -92,7 +96,8 @@ def _gather_rows(G, until_k, styles, temp_shapes, full=()):
     for r, w in specs:
         out[r] = flat[off:off + n * w].view(n, w)
         off += n * w
-    return out
+    block = flat[:len(lead) * n * styles.shape[2]].view(len(lead), n, styles.shape[2]) if lead else None
+    return out, block
 
 
 def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", delta=None,
@@ -103,34 +108,41 @@ def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", del
     tensor: only the rows that carry `delta` ([N or 1, len(trainable), 512]) require grad, so the
     backward skips every style gradient find_direction does not use and stops below the first
     trainable layer.  styles2[:, r] = styles[:, r] + delta[:, j] for r = trainable[j] (find_direction.py:307-308).
+    The trainable rows are gathered as one [T, N, 512] block and delta is added to it in one op: per row
+    (a select, an add and its batch sum), the backward cost ~5 small kernels a row on the critical path.
     """
     x = img = None
     row = 0
-    gathered = _gather_rows(G, until_k, styles, temp_shapes, full=set(trainable) if delta is not None else ())
+    trainable = list(trainable)
+    gathered, block = _gather_rows(G, until_k, styles, temp_shapes, full=set(trainable) if delta is not None else (),
+                                   lead=trainable if delta is not None else ())
+    edited = None
+    if block is not None:
+        edited = (block + delta.reshape(-1, len(trainable), block.shape[2]).transpose(0, 1)).unbind(0)
     for k, res in enumerate(G.synthesis.block_resolutions):
         if k > until_k:
             continue
-        block = getattr(G.synthesis, f"b{res}")
+        block_k = getattr(G.synthesis, f"b{res}")
         width = 2 if res == 4 else 3
         rows = []
         for j in range(width):
             r = row + j
             w = gathered[r]
             if delta is not None and r in trainable:
-                w = w + delta[:, trainable.index(r)]
+                w = edited[trainable.index(r)] if edited is not None else w + delta[:, trainable.index(r)]
             rows.append(w)
         shapes = temp_shapes[k]
-        if block.in_channels == 0:
-            x = block.const.to(torch.float32).unsqueeze(0).repeat([styles.shape[0], 1, 1, 1])
+        if block_k.in_channels == 0:
+            x = block_k.const.to(torch.float32).unsqueeze(0).repeat([styles.shape[0], 1, 1, 1])
             w1 = rows[0][..., :shapes[0]]
         else:
-            x = block.conv0(x, rows[0][..., :shapes[0]], noise_mode=noise_mode)
+            x = block_k.conv0(x, rows[0][..., :shapes[0]], noise_mode=noise_mode)
             w1 = rows[1][..., :shapes[1]]
         if img is not None:
-            img = upfirdn2d.upsample2d(img, block.resample_filter)
+            img = upfirdn2d.upsample2d(img, block_k.resample_filter)
         # conv1 + ToRGB as one Function: the backward sums the block output's two gradients (ToRGB and the next
         # block's conv0) inside conv1's epilogue backward
-        x, y = block.conv1_torgb(x, w1, rows[-1][..., :shapes[2]], noise_mode=noise_mode)
+        x, y = block_k.conv1_torgb(x, w1, rows[-1][..., :shapes[2]], noise_mode=noise_mode)
         img = img.add_(y) if img is not None else y
         row += width
     return img
