@@ -125,9 +125,9 @@ class ToRGBLayer(torch.nn.Module):
         self.weight_gain = 1 / math.sqrt(in_channels * kernel_size * kernel_size)
         self._w2d = _SpecCache()
 
-    def fn_args(self, x, w):
-        """The ToRGBFn argument tuple of forward(x, w)."""
-        styles = self.affine(w) * self.weight_gain
+    def fn_args(self, x, w, scaled=False):
+        """The ToRGBFn argument tuple of forward(x, w); scaled: w is already affine(w) * weight_gain."""
+        styles = w if scaled else self.affine(w) * self.weight_gain
         w2d = self._w2d.get(_version_key(self.weight), lambda: self.weight.detach()[:, :, 0, 0].float().contiguous())
         clamp = float(self.conv_clamp) if self.conv_clamp is not None else -1.0
         return x.float(), styles.float(), w2d, self.bias.detach().float().contiguous(), clamp
@@ -166,10 +166,12 @@ class SynthesisBlock(torch.nn.Module):
         self.torgb = ToRGBLayer(out_channels, img_channels, w_dim, conv_clamp=conv_clamp)
         self.num_torgb += 1
 
-    def conv1_torgb(self, x, w1, w_rgb, noise_mode="random"):
+    def conv1_torgb(self, x, w1, w_rgb, noise_mode="random", rgb_scaled=False):
         """conv1(x, w1) and the ToRGB of its output as one autograd Function (modconv.ModConvToRGBFn, whose
-        backward fuses the two gradients of the block output): returns (x, rgb) = (conv1 output, ToRGB output)."""
-        return modconv.ModConvToRGBFn.apply(*self.conv1.fn_args(x, w1, noise_mode), *self.torgb.fn_args(x, w_rgb)[1:])
+        backward fuses the two gradients of the block output): returns (x, rgb) = (conv1 output, ToRGB output).
+        rgb_scaled: w_rgb is already the ToRGB styles (affine(w_rgb) * weight_gain, see utils._gather_rows)."""
+        return modconv.ModConvToRGBFn.apply(*self.conv1.fn_args(x, w1, noise_mode),
+                                            *self.torgb.fn_args(x, w_rgb, scaled=rgb_scaled)[1:])
 
     def forward(self, x, img, ws, force_fp32=False, fused_modconv=None, **layer_kwargs):
         rows = iter(ws.unbind(dim=1))

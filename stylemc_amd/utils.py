@@ -64,12 +64,14 @@ def generate_image(G, until_k, styles, temp_shapes, noise_mode="const", device=N
 _GATHER_IDX = {}
 
 
-def _gather_rows(G, until_k, styles, temp_shapes, full=(), lead=()):
+def _gather_rows(G, until_k, styles, temp_shapes, full=(), lead=(), gains=None):
     """Every S row a layer of the synthesis reads, cut to the layer's width, as contiguous [N, width] tensors from
     ONE gather (index_select) -- the per-layer views styles[:, r, :width] would each cost a copy kernel (the layers
     take contiguous style rows).  Returns ({row: tensor}, block): rows in `full` keep all columns (the trainable
     rows: delta is added before the cut); rows past until_k are not gathered.  The rows of `lead` (all of them
-    gathered, in `full`) come first, in that order, and `block` is them as one [len(lead), N, C] tensor (else None)."""
+    gathered, in `full`) come first, in that order, and `block` is them as one [len(lead), N, C] tensor (else None).
+    Rows in `gains` ({row: float}, not in `lead`) come next and are returned times their gain, all in one multiply
+    (the ToRGB layers' weight_gain: per layer, one small kernel each)."""
     n = styles.shape[0]
     specs = []
     row = 0
@@ -82,16 +84,26 @@ def _gather_rows(G, until_k, styles, temp_shapes, full=(), lead=()):
         row += width
     rows = {r for r, _ in specs}
     lead = tuple(lead) if lead and all(r in rows and r in full for r in lead) else ()
-    specs = [sp for r in lead for sp in specs if sp[0] == r] + [sp for sp in specs if sp[0] not in lead]
+    gains = {r: g for r, g in (gains or {}).items() if r in rows and r not in lead}
+    scaled = [sp for sp in specs if sp[0] in gains]
+    specs = ([sp for r in lead for sp in specs if sp[0] == r] + scaled +
+             [sp for sp in specs if sp[0] not in lead and sp[0] not in gains])
     styles = styles.contiguous()
-    key = (n, styles.shape[1], styles.shape[2], tuple(specs), styles.device)
-    idx = _GATHER_IDX.get(key)
-    if idx is None:
+    key = (n, styles.shape[1], styles.shape[2], tuple(specs), styles.device, tuple(sorted(gains.items())))
+    cached = _GATHER_IDX.get(key)
+    if cached is None:
         nr, c = styles.shape[1], styles.shape[2]
         base = torch.arange(n).view(n, 1) * (nr * c)
         idx = torch.cat([(base + r * c + torch.arange(w).view(1, w)).reshape(-1) for r, w in specs]).to(styles.device)
-        _GATHER_IDX[key] = idx
+        # float32 gains, element by element: the product is the layer's own `styles * weight_gain`, bit for bit
+        gvec = torch.cat([torch.full((n * w,), gains[r], dtype=torch.float32) for r, w in scaled]).to(styles.device) \
+            if scaled else None
+        cached = _GATHER_IDX[key] = (idx, gvec)
+    idx, gvec = cached
     flat = styles.reshape(-1).index_select(0, idx)
+    if gvec is not None:  # in place: `flat` is this call's own gather
+        s0 = len(lead) * n * styles.shape[2]
+        flat[s0:s0 + gvec.numel()].mul_(gvec)
     out, off = {}, 0
     for r, w in specs:
         out[r] = flat[off:off + n * w].view(n, w)
@@ -114,8 +126,14 @@ def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", del
     x = img = None
     row = 0
     trainable = list(trainable)
+    gains = {}
+    row = 0
+    for k, res in enumerate(G.synthesis.block_resolutions):
+        row += 2 if res == 4 else 3
+        gains[row - 1] = getattr(G.synthesis, f"b{res}").torgb.weight_gain
+    row = 0
     gathered, block = _gather_rows(G, until_k, styles, temp_shapes, full=set(trainable) if delta is not None else (),
-                                   lead=trainable if delta is not None else ())
+                                   lead=trainable if delta is not None else (), gains=gains)
     edited = None
     if block is not None:
         edited = (block + delta.reshape(-1, len(trainable), block.shape[2]).transpose(0, 1)).unbind(0)
@@ -142,7 +160,8 @@ def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", del
             img = upfirdn2d.upsample2d(img, block_k.resample_filter)
         # conv1 + ToRGB as one Function: the backward sums the block output's two gradients (ToRGB and the next
         # block's conv0) inside conv1's epilogue backward
-        x, y = block_k.conv1_torgb(x, w1, rows[-1][..., :shapes[2]], noise_mode=noise_mode)
+        x, y = block_k.conv1_torgb(x, w1, rows[-1][..., :shapes[2]], noise_mode=noise_mode,
+                                   rgb_scaled=(row + width - 1) not in trainable or delta is None)
         img = img.add_(y) if img is not None else y
         row += width
     return img
