@@ -15,6 +15,9 @@ void set_error(const char* fmt, ...);
 int conv_gemm_aux(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h, int y_w,
                   const smc_conv_phase* phases, int nphases, const float* s_in, const smc_conv_epilogue* epi,
                   float* workspace, int64_t workspace_bytes, void* stream);
+// smc_conv_gemm_workspace_size for conv_gemm_aux (its split-K plan differs)
+int64_t conv_gemm_aux_workspace_size(int n, int cin, int cout, int y_h, int y_w, const smc_conv_phase* phases,
+                                     int nphases);
 int check_launch(const char* what);
 int device_cu_count();
 

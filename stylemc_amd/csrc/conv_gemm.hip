@@ -1288,7 +1288,7 @@ int pick_cfg(int cout, Cfg* c) {
 }
 
 // Shared by the workspace query and the launch so both agree on the split.
-int plan_split(int n, int cin, int cout, const smc_conv_phase* ph, int nph, const Cfg& c) {
+int plan_split(int n, int cin, int cout, const smc_conv_phase* ph, int nph, const Cfg& c, int target_per_cu = 2) {
     int64_t blocks = 0;
     int min_ks = 1 << 30;
     for (int i = 0; i < nph; ++i) {
@@ -1297,7 +1297,7 @@ int plan_split(int n, int cin, int cout, const smc_conv_phase* ph, int nph, cons
         const int ks = ph[i].ntaps * (cin / BK);
         if (ks < min_ks) min_ks = ks;
     }
-    const int64_t target = 2LL * smc::device_cu_count();
+    const int64_t target = (int64_t)target_per_cu * smc::device_cu_count();
     if (blocks >= target) return 1;
     int s = (int)smc::ceil_div(target, blocks > 0 ? blocks : 1);
     int cap = min_ks / 4;
@@ -1418,8 +1418,15 @@ int validate(const float* x, int n, int cin, int in_h, int in_w, float* y, int c
 
 }  // namespace
 
-SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, int y_w, const smc_conv_phase* phases,
-                                             int nphases) {
+namespace {
+
+// Split-K target of the IR-SE50 executor's GEMMs (TAG 1), in workgroups per CU: its 7..28-px stages are
+// latency-bound chains of small GEMMs where more, shorter splits pay (tools/prof_irse.py, IR-SE50 pair
+// fwd(8) + bwd(4): 2 -> 4.34 ms, 4 -> 4.16; 1 -> 4.99).  The synthesis keeps 2.
+constexpr int kSplitPerCuAux = 4;
+
+int64_t workspace_size_impl(int n, int cin, int cout, int y_h, int y_w, const smc_conv_phase* phases, int nphases,
+                            int split_per_cu) {
     Cfg c;
     if (pick_cfg(cout, &c) < 0 || cin % BK != 0 || nphases < 1 || nphases > 4 || !phases) return 0;
     int s;
@@ -1432,8 +1439,8 @@ SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, 
              convt_fusable(cin, cout, (y_h - 1) / 2, (y_w - 1) / 2, y_h, y_w, phases, nphases, nullptr, nullptr))
         s = plan_split_convt(n, cin, cout, (y_h - 1) / 2, (y_w - 1) / 2);
     else
-        s = plan_split(n, cin, cout, phases, nphases, c);
-    if (cout % 64 == 0) s = std::max(s, plan_split(n, cin, cout, phases, nphases, Cfg{64, 64}));  // small tile
+        s = plan_split(n, cin, cout, phases, nphases, c, split_per_cu);
+    if (cout % 64 == 0) s = std::max(s, plan_split(n, cin, cout, phases, nphases, Cfg{64, 64}, split_per_cu));  // small tile
     int64_t bytes = s > 1 ? (int64_t)s * n * cout * y_h * y_w * (int64_t)sizeof(float) : 0;
     // the LDS-DMA kernel's per-sample weights when the input is style-scaled (the query does not know
     // whether it will be: reserve whenever the shape qualifies)
@@ -1444,6 +1451,13 @@ SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, 
         bytes = ((bytes + 255) / 256) * 256 +
                 std::max(wsample_floats(n, cin, cout, phases, nphases), pre) * (int64_t)sizeof(float);
     return bytes;
+}
+
+}  // namespace
+
+SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, int y_w, const smc_conv_phase* phases,
+                                             int nphases) {
+    return workspace_size_impl(n, cin, cout, y_h, y_w, phases, nphases, 2);
 }
 
 namespace {
@@ -1472,7 +1486,7 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     const bool t_per_sample = convt_lds && s_in && ((int64_t)(in_h + 1) * (in_w + 1)) % tl.bm != 0;
     const int nsplit = convt_lds ? plan_split_convt_lds(n, cin, cout, in_h, in_w, tl, t_per_sample)
                                  : fused_t ? plan_split_convt(n, cin, cout, in_h, in_w)
-                                           : plan_split(n, cin, cout, phases, nphases, c);
+                                           : plan_split(n, cin, cout, phases, nphases, c, tag ? kSplitPerCuAux : 2);
     const int64_t plane_elems = (int64_t)n * cout * y_h * y_w;
     if (nsplit > 1) {
         const int64_t need = nsplit * plane_elems * (int64_t)sizeof(float);
@@ -1670,6 +1684,11 @@ SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w
 }
 
 namespace smc {
+int64_t conv_gemm_aux_workspace_size(int n, int cin, int cout, int y_h, int y_w, const smc_conv_phase* phases,
+                                     int nphases) {
+    return workspace_size_impl(n, cin, cout, y_h, y_w, phases, nphases, kSplitPerCuAux);
+}
+
 int conv_gemm_aux(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h, int y_w,
                   const smc_conv_phase* phases, int nphases, const float* s_in, const smc_conv_epilogue* epi,
                   float* workspace, int64_t workspace_bytes, void* stream) {

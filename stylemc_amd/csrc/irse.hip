@@ -249,7 +249,7 @@ int max_channels(const smc_irse_net& net) {
 int64_t conv_ws_need(const smc_irse_net& net, int n) {
     int64_t m = 0;
     auto q = [&](int cin, int cout, int yh, int yw, const smc_conv_phase* ph, int nph) {
-        m = std::max(m, smc_conv_gemm_workspace_size(n, cin, cout, yh, yw, ph, nph));
+        m = std::max(m, smc::conv_gemm_aux_workspace_size(n, cin, cout, yh, yw, ph, nph));
     };
     q(net.stem_cin, net.stem_cout, net.in_h, net.in_w, &net.stem_fwd, 1);
     q(net.stem_cout, net.stem_cin, net.in_h, net.in_w, &net.stem_bwd, 1);
