@@ -228,6 +228,8 @@ class TextTransformer(nn.Module):
             linear(h, p["in_t"], blk.attn.in_proj_bias, qkv)
             _hip.call("smc_attention_causal_fwd_f32", qkv.data_ptr(), o.data_ptr(), B, L, blk.heads, D // blk.heads,
                       1.0 / math.sqrt(D // blk.heads), st)
+            # in place (C aliases the residual): allowed by the smc_linear_f32 contract in include/stylemc_hip.h,
+            # pinned by tests/test_gpu_vit.py::test_linear_epilogues ("bias+residual in place", split-K shapes)
             linear(o, p["out_t"], blk.attn.out_proj.bias, x, residual=x)
             _hip.call("smc_layernorm_fwd_f32", x.data_ptr(), D, blk.ln_2.weight.data_ptr(), blk.ln_2.bias.data_ptr(),
                       h.data_ptr(), D, None, None, M, D, blk.ln_2.eps, st)

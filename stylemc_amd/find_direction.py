@@ -125,8 +125,10 @@ class DirectionFinder:
     def __init__(self, G, styles_array, clip_losses, id_loss, resolution=1024, batch_size=4, learning_rate=1.5,
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
-                 overlap=True, batch_losses=True, prefetch_orig=True):
+                 overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None):
         self.G = G
+        # how the side / prefetch streams are made (default: torch's stream pool); tools/stream_ab.py A/Bs it
+        self.stream_factory = stream_factory or (lambda dev: torch.cuda.Stream(device=dev))
         self.synth_fn = synth_fn or utils.generate_image_rows   # (G, until_k, styles, shapes, noise, delta=)
         self.overlap = overlap                                  # original-image branch on a second stream
         # software pipelining across iterations: the NEXT iteration's original-image synthesis (it depends only
@@ -284,7 +286,7 @@ class DirectionFinder:
         if not (self.overlap and self.device.type == "cuda"):
             return None
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            self._side = self.stream_factory(self.device)
         return self._side
 
     def _shard(self, i):
@@ -299,7 +301,7 @@ class DirectionFinder:
         if b <= a:
             return
         if getattr(self, "_pre", None) is None:
-            self._pre = torch.cuda.Stream(device=self.device)
+            self._pre = self.stream_factory(self.device)
         self._pre.wait_event(self._fwd_done)
         with torch.cuda.stream(self._pre), torch.no_grad():
             orig = self.synth_fn(self.G, self.until_k, self.styles_array[a:b], self.temp_shapes, self.noise_mode)
@@ -410,12 +412,19 @@ def build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip
                       clip_weights=None, text_features=None, bpe_path=None, synthetic_weights=False):
     """init_clip_loss (find_direction.py:100-122) for the default loss: [(CLIPLoss, weight)], 'double' ->
     ViT-B/32 at 1 + ViT-B/16 at 0.5 (:163-166).  clip_weights / text_features: {'small'|'large': ...}."""
-    from .clip_loss import CLIPLoss
+    from .clip_loss import MODEL_NAMES, CLIPLoss
     if clip_loss_type != "default":
         raise NotImplementedError("the StyleGAN-NADA losses (clip_loss_nada.py) are outside the hot path")
     kinds = [("small", 1.0), ("large", 0.5)] if clip_type == "double" else [(clip_type, 1.0)]
-    clip_weights = clip_weights or {}
-    text_features = text_features or {}
+    clip_weights = {k: v for k, v in (clip_weights or {}).items() if v}
+    text_features = {k: v for k, v in (text_features or {}).items() if v is not None}
+    if synthetic_weights and (clip_weights or text_features):
+        # real weights for one model and seeded ones for another would give a meaningless mixed direction
+        missing = [MODEL_NAMES[k] for k, _ in kinds if k not in clip_weights]
+        if missing:
+            raise ValueError(f"--clip_type {clip_type}: CLIP weights were given, but not for {', '.join(missing)} "
+                             f"(--clip_weights for ViT-B/32, --clip_weights_large for ViT-B/16)")
+        synthetic_weights = False
     out = []
     for kind, w in kinds:
         path = clip_weights.get(kind)

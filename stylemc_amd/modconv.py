@@ -68,12 +68,15 @@ class PackedConv:
 
     def wino_weights(self, flip):
         """Winograd F(2x2, 3x3) transformed taps (smc_wino_weights_f32) of the 3x3 'same' conv, built once on the
-        weights' device: flip 0 = the forward, 1 = the data gradient."""
+        weights' device: flip 0 = the forward, 1 = the data gradient.  LayerSpec builds both eagerly for the layers
+        that take the Winograd path; a transform built here later is waited for before it is returned (the first
+        caller may be on a side stream while the next launch that reads it is on another one)."""
         if flip not in self._wino:
             W = self.wk_bwd  # [t][o][i] -> back to [o][i][3][3] on the same device
             w = W.reshape(3, 3, self.cout, self.cin).permute(2, 3, 0, 1).contiguous()
             uw = torch.empty(16 * self.cin * self.cout, device=w.device, dtype=torch.float32)
             _hip.call("smc_wino_weights_f32", w.data_ptr(), self.cout, self.cin, flip, uw.data_ptr(), _hip.stream())
+            torch.cuda.current_stream(w.device).synchronize()
             self._wino[flip] = uw
         return self._wino[flip]
 
@@ -162,7 +165,7 @@ def _epilogue(mode, d=None, noise=None, noise_nstride=0, strength=None, bias=Non
 class LayerSpec:
     """Everything the modconv kernels need about one frozen layer (built once per SynthesisLayer)."""
 
-    def __init__(self, weight, bias, up, resample_filter, demodulate=True, act="lrelu", alpha=0.2):
+    def __init__(self, weight, bias, up, resample_filter, demodulate=True, act="lrelu", alpha=0.2, resolution=None):
         self.packed = PackedConv(weight, up)
         self.bias = bias.detach().float().contiguous() if bias is not None else None
         self.up = up
@@ -170,6 +173,17 @@ class LayerSpec:
         self.demodulate = demodulate
         self.act = act
         self.alpha = alpha
+        P = self.packed
+        if weight.is_cuda:
+            # the spec is built lazily, on whichever stream first reaches the layer (find_direction's first step
+            # runs the original-image synthesis on a side stream): build the Winograd transforms of a Winograd
+            # layer now, and let every packing kernel finish before another stream can read the packed weights
+            if resolution is not None and up == 1 and P.k == 3:
+                if wino_ok(1, P.cin, P.cout, resolution, resolution):
+                    P.wino_weights(0)
+                if wino_ok(1, P.cout, P.cin, resolution, resolution):
+                    P.wino_weights(1)
+            torch.cuda.current_stream(weight.device).synchronize()
 
 
 def _noise_args(noise):

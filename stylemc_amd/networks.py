@@ -91,7 +91,8 @@ class SynthesisLayer(torch.nn.Module):
         alpha = _bias_act.activation_funcs[self.activation].def_alpha
         return self._spec.get(_version_key(self.weight, self.bias, self.resample_filter),
                               lambda: modconv.LayerSpec(self.weight, self.bias, self.up, self.resample_filter,
-                                                        demodulate=True, act=self.activation, alpha=alpha))
+                                                        demodulate=True, act=self.activation, alpha=alpha,
+                                                        resolution=self.resolution))
 
     def fn_args(self, x, w, noise_mode="random", gain=1):
         """The ModConvFn argument tuple of forward(x, w, noise_mode, gain=gain)."""
@@ -128,9 +129,15 @@ class ToRGBLayer(torch.nn.Module):
     def fn_args(self, x, w, scaled=False):
         """The ToRGBFn argument tuple of forward(x, w); scaled: w is already affine(w) * weight_gain."""
         styles = w if scaled else self.affine(w) * self.weight_gain
-        w2d = self._w2d.get(_version_key(self.weight), lambda: self.weight.detach()[:, :, 0, 0].float().contiguous())
+        w2d = self._w2d.get(_version_key(self.weight), self._pack_w2d)
         clamp = float(self.conv_clamp) if self.conv_clamp is not None else -1.0
         return x.float(), styles.float(), w2d, self.bias.detach().float().contiguous(), clamp
+
+    def _pack_w2d(self):
+        w2d = self.weight.detach()[:, :, 0, 0].float().contiguous()
+        if w2d.is_cuda:  # built on whichever stream first reaches the layer; other streams read it right after
+            torch.cuda.current_stream(w2d.device).synchronize()
+        return w2d
 
     def forward(self, x, w, fused_modconv=True):
         return modconv.ToRGBFn.apply(*self.fn_args(x, w))

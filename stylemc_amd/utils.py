@@ -4,13 +4,10 @@
   generate_image  (utils.py:161-216) block loop up to `until_k`; `device` is optional here (the
                                      reference's find_direction.py:309,312 omits it -> TypeError there)
   get_temp_shapes (utils.py:100-120) style widths per block; replaces each affine by Identity
-  split_ws        (utils.py:77-87), get_styles (utils.py:123-158), get_mean_std (utils.py:90-97),
-  num_range       (utils.py:64-74)
+  split_ws        (utils.py:77-87), get_styles (utils.py:123-158), get_mean_std (utils.py:90-97)
 The feature-blending branches of generate_image (use_blending, cv2 masks) are out of scope
  and raise NotImplementedError.
 """
-import re
-
 import torch
 
 from .torch_utils.ops import upfirdn2d
@@ -124,13 +121,18 @@ def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", del
     (a select, an add and its batch sum), the backward cost ~5 small kernels a row on the critical path.
     """
     x = img = None
-    row = 0
     trainable = list(trainable)
+    # the ToRGB rows are handed over pre-scaled (affine(w) * weight_gain with affine = Identity, applied in the
+    # gather) only when get_temp_shapes has replaced every ToRGB affine; with an intact affine the layer applies
+    # affine and gain itself, as generate_image does
+    rgb_prescaled = all(isinstance(getattr(G.synthesis, f"b{res}").torgb.affine, torch.nn.Identity)
+                        for res in G.synthesis.block_resolutions)
     gains = {}
     row = 0
     for k, res in enumerate(G.synthesis.block_resolutions):
         row += 2 if res == 4 else 3
-        gains[row - 1] = getattr(G.synthesis, f"b{res}").torgb.weight_gain
+        if rgb_prescaled:
+            gains[row - 1] = getattr(G.synthesis, f"b{res}").torgb.weight_gain
     row = 0
     gathered, block = _gather_rows(G, until_k, styles, temp_shapes, full=set(trainable) if delta is not None else (),
                                    lead=trainable if delta is not None else (), gains=gains)
@@ -161,7 +163,7 @@ def generate_image_rows(G, until_k, styles, temp_shapes, noise_mode="const", del
         # conv1 + ToRGB as one Function: the backward sums the block output's two gradients (ToRGB and the next
         # block's conv0) inside conv1's epilogue backward
         x, y = block_k.conv1_torgb(x, w1, rows[-1][..., :shapes[2]], noise_mode=noise_mode,
-                                   rgb_scaled=(row + width - 1) not in trainable or delta is None)
+                                   rgb_scaled=rgb_prescaled and ((row + width - 1) not in trainable or delta is None))
         img = img.add_(y) if img is not None else y
         row += width
     return img
@@ -219,10 +221,3 @@ def get_mean_std(device):
     mean = torch.as_tensor((0.48145466, 0.4578275, 0.40821073), dtype=torch.float, device=device).view(-1, 1, 1)
     std = torch.as_tensor((0.26862954, 0.26130258, 0.27577711), dtype=torch.float, device=device).view(-1, 1, 1)
     return mean, std
-
-
-def num_range(s):
-    m = re.match(r"^(\d+)-(\d+)$", s)
-    if m:
-        return list(range(int(m.group(1)), int(m.group(2)) + 1))
-    return [int(v) for v in s.split(",")]

@@ -19,6 +19,16 @@ from . import utils
 from .synthetic import seed_latents
 
 
+def parse_seeds(text):
+    """--seeds as generate_w.py takes them (utils.py:64-74 num_range): comma-separated items, each a seed or an
+    inclusive range 'a-b'."""
+    out = []
+    for item in str(text).split(","):
+        lo, sep, hi = item.strip().partition("-")
+        out.extend(range(int(lo), int(hi) + 1) if sep else [int(lo)])
+    return out
+
+
 @torch.no_grad()
 def seeds_to_w(G, seeds, truncation_psi=1.0, device="cuda"):
     z = seed_latents(seeds, G.z_dim).to(device)
@@ -42,7 +52,7 @@ def _cli():
 
     @cli.command("generate_w")
     @click.option("--network", "network_pkl", default="synthetic")
-    @click.option("--seeds", type=utils.num_range, required=True)
+    @click.option("--seeds", type=parse_seeds, required=True)
     @click.option("--trunc", "truncation_psi", type=float, default=1.0, show_default=True)
     @click.option("--out_file", type=str, default="encoder4editing/projected_w.npz")
     @click.option("--resolution", type=int, default=1024)

@@ -94,3 +94,27 @@ def test_find_direction_ffhq1024_torch_losses_vs_oracle():
     """BASELINE config 2: CLIP ViT-B/32 and IR-SE50 on PyTorch-ROCm ops (--clip-impl/--id-impl torch), the
     synthesis on the HIP kernels, forward and backward through the whole loop."""
     _check(*_run_pair(1024, 32768, n_items=3, bs=2, iters=2, impl="torch"), max_err=1e-2)
+
+
+def test_first_step_overlap_matches_serial():
+    """The first iteration builds every layer's packed / Winograd weights lazily, on whichever stream reaches
+    the layer first (the original-image synthesis runs on a side stream); the main stream must never read a
+    half-written transform.  Fresh generators, first step with the three-stream schedule vs fully serial:
+    the gradients agree bit for bit (same kernels, same inputs)."""
+    from stylemc_amd import build, networks
+    from stylemc_amd.clip_loss import CLIPLoss
+    from stylemc_amd.find_direction import DirectionFinder, initial_delta
+    from stylemc_amd.id_loss import IDLoss
+    build.build(verbose=False)
+    text = synthetic.text_direction("a", "b")
+    styles = synthetic.synthetic_styles(4, seed=5).to(DEV)
+    cfg = synthetic.generator_config(resolution=256)
+    grads = []
+    for overlap in (True, False):
+        G = networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=DEV)
+        f = DirectionFinder(G, styles, [(CLIPLoss(DEV, text_features=text, synthetic_weights=True, seed=4), 1.0)],
+                            IDLoss(device=DEV, weights=None, seed=3), resolution=256, batch_size=4, n_epochs=2,
+                            seed=0, init_delta=initial_delta(0, 0.01), overlap=overlap)
+        grads.append(f.step()["grad"].cpu())
+    assert torch.isfinite(grads[0]).all()
+    assert torch.equal(grads[0], grads[1]), (grads[0] - grads[1]).abs().max()
