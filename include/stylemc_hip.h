@@ -221,6 +221,15 @@ int smc_clip_unprocess_f32(const float* img, int n, int channels, int in_h, int 
                            const float* mean, const float* std_, float* y, void* stream);
 int smc_clip_unprocess_bwd_f32(const float* img, const float* dy, int n, int channels, int in_h, int in_w, int out_h,
                                int out_w, const float* mean, const float* std_, float* dimg, void* stream);
+/* StyleGAN-NADA CLIP preprocessing (clip_loss_nada.py:72-75 `preprocess`, applied at :109-111 and :225):
+ * torchvision Normalize(mean=-1, std=2) -> Resize(out, BICUBIC) -> CenterCrop(out) -> Normalize(CLIP mean, std),
+ * no clamp: y = (bicubic((img + 1) / 2, out) - mean[c]) / std[c].  Same shapes / backward contract as
+ * smc_clip_unprocess_f32 (square input, so the crop is the identity). */
+int smc_clip_preprocess_nada_f32(const float* img, int n, int channels, int in_h, int in_w, int out_h, int out_w,
+                                 const float* mean, const float* std_, float* y, void* stream);
+int smc_clip_preprocess_nada_bwd_f32(const float* img, const float* dy, int n, int channels, int in_h, int in_w,
+                                     int out_h, int out_w, const float* mean, const float* std_, float* dimg,
+                                     void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * CLIP ViT image tower (replaces the third-party openai/CLIP VisionTransformer that the reference

@@ -29,9 +29,11 @@ def cosine_lr(lr0, it, total):
 
 def find_direction(G, styles_array, clip_loss, id_loss, temp_shapes, until_k, batch_size=4, learning_rate=1.5,
                    n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
-                   seed=0, max_iterations=None, log=None, init_delta=None, init_direction=None):
+                   seed=0, max_iterations=None, log=None, init_delta=None, init_direction=None, clip_loss2=None,
+                   clip_loss_type="default", text_prompt=None, negative_text_prompt=None):
     """init_direction: a resumed [1, 26, 512] styles_direction (find_direction.py:266-271); its T rows are the
-    start delta and the whole tensor is added to the styles (styles2 = styles + styles_direction, :307-308)."""
+    start delta and the whole tensor is added to the styles (styles2 = styles + styles_direction, :307-308).
+    clip_loss2 / clip_loss_type / prompts: compute_loss's --clip_type double and NADA options (:150-169)."""
     T = S_TRAINABLE_SPACE_CHANNELS
     rng = np.random.RandomState(seed)
     mean, std = get_mean_std()
@@ -61,7 +63,9 @@ def find_direction(G, styles_array, clip_loss, id_loss, temp_shapes, until_k, ba
             with torch.no_grad():
                 _, original_img = generate_image(G, until_k, styles, temp_shapes, noise_mode)
             loss, parts = compute_loss(img, original_img, styles, styles2, clip_loss, id_loss, mean, std,
-                                       identity_loss_coef, clip_loss_coef, l2_reg_coef, T)
+                                       identity_loss_coef, clip_loss_coef, l2_reg_coef, T, clip_loss2=clip_loss2,
+                                       clip_loss_type=clip_loss_type, text_prompt=text_prompt,
+                                       negative_text_prompt=negative_text_prompt)
             delta.grad = None
             loss.backward()
             with torch.no_grad():

@@ -38,15 +38,19 @@ def render_projected_w(G, ws, noise_mode="const"):
 
 @torch.no_grad()
 def render_pairs(G, styles, direction, change_power, temp_shapes, noise_mode="const", mapper=None,
-                 use_whitelist=False):
+                 use_whitelist=False, G2=None, temp_shapes2=None):
+    """G2: --network2, the edited image (j == 1) from the second generator (:80-86,168-170)."""
     out = []
     for i in range(styles.shape[0]):
         imgs = []
-        for p in [0, change_power]:
+        for j, p in enumerate([0, change_power]):
             if mapper is not None:
                 direction = mapper_direction(mapper, styles[i], use_whitelist)
             styles += direction * p
-            _, img = generate_image(G, 100, styles[[i]], temp_shapes, noise_mode)
+            if G2 is not None and j == 1:
+                _, img = generate_image(G2, 100, styles[[i]], temp_shapes2, noise_mode)
+            else:
+                _, img = generate_image(G, 100, styles[[i]], temp_shapes, noise_mode)
             imgs.append(to_uint8(img)[0])
             styles -= direction * p
         out.append(imgs)

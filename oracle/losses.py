@@ -11,7 +11,12 @@
   IRSE50 / IDLoss           <- id_loss/model_irse.py:10-49, id_loss/helpers.py:29-119,
                                id_loss/id_loss.py:7-39
   compute_loss              <- find_direction.py:172-200 (landmarks coefficient 0: that branch runs
-                               under torch.no_grad, find_direction.py:90, and adds no gradient)
+                               under torch.no_grad, find_direction.py:90, and adds no gradient);
+                               clip_loss_type 'nada' / 'nada_global' <- :100-114,150-157
+  nada_preprocess / CLIPLossNADA <- clip_loss_nada.py:72-75 (torchvision Normalize(-1, 2) + CLIP Resize /
+                               CenterCrop / Normalize, restated -> parity unpinned for that step),
+                               :126-153 (template text direction), :177-229 (directional, angle, global
+                               losses), :324-346 (forward)
 """
 import math
 
@@ -165,6 +170,78 @@ class CLIPLoss(nn.Module):
         return (len(src_image) - cos.sum()) / len(src_image)
 
 
+# ----------------------------------------------------------------------------- StyleGAN-NADA losses
+
+
+NADA_TEMPLATES = [
+    'a photo of a {}.', 'a rendering of a {}.', 'a cropped photo of the {}.', 'the photo of a {}.',
+    'a photo of a clean {}.', 'a photo of a dirty {}.', 'a dark photo of the {}.', 'a photo of my {}.',
+    'a photo of the cool {}.', 'a close-up photo of a {}.', 'a bright photo of the {}.', 'a cropped photo of a {}.',
+    'a photo of the {}.', 'a good photo of the {}.', 'a photo of one {}.', 'a close-up photo of the {}.',
+    'a rendition of the {}.', 'a photo of the clean {}.', 'a rendition of a {}.', 'a photo of a nice {}.',
+    'a good photo of a {}.', 'a photo of the nice {}.', 'a photo of the small {}.', 'a photo of the weird {}.',
+    'a photo of the large {}.', 'a photo of a cool {}.', 'a photo of a small {}.',
+]
+
+
+def nada_preprocess(img, mean, std, size=224):
+    """clip_loss_nada.py:72-75: Normalize(mean=-1, std=2) -> Resize(size, BICUBIC) -> CenterCrop -> Normalize."""
+    x = (img - (-1.0)) / 2.0
+    return (resize_center_crop(x, size) - mean) / std
+
+
+class CLIPLossNADA(nn.Module):
+    """clip_loss_nada.CLIPLoss restated around an image encoder and an E_T(list of strings) callable."""
+
+    def __init__(self, visual, text_encoder, lambda_direction=1.0, lambda_global=0.0, lambda_manifold=0.0,
+                 logit_scale=math.log(100.0)):
+        super().__init__()
+        self.visual = visual
+        self.text_encoder = text_encoder
+        self.lambda_direction, self.lambda_global, self.lambda_manifold = lambda_direction, lambda_global, lambda_manifold
+        self.logit_scale = torch.tensor(logit_scale, dtype=torch.float32)
+        self.mean, self.std = get_mean_std()
+        self.target_direction = None
+        self.src_text_features = None
+        self.target_text_features = None
+
+    def get_text_features(self, class_str):
+        f = self.text_encoder([t.format(class_str) for t in NADA_TEMPLATES]).detach()
+        return f / f.norm(dim=-1, keepdim=True)
+
+    def compute_text_direction(self, source_class, target_class):
+        d = (self.get_text_features(target_class) - self.get_text_features(source_class)).mean(0, keepdim=True)
+        return d / d.norm(dim=-1, keepdim=True)
+
+    def image_features(self, img):
+        f = self.visual(nada_preprocess(img, self.mean, self.std))
+        return f / f.norm(dim=-1, keepdim=True)
+
+    def forward(self, src_img, source_class, target_img, target_class):
+        loss = 0.0
+        if self.lambda_global:
+            t = self.text_encoder([f"a {target_class}"]).detach()
+            t = t / t.norm(dim=1, keepdim=True)
+            logits = self.logit_scale.exp() * self.image_features(target_img) @ t.t()
+            loss = loss + self.lambda_global * (1.0 - logits / 100).mean()
+        if self.lambda_direction:
+            if self.target_direction is None:
+                self.target_direction = self.compute_text_direction(source_class, target_class)
+            edit = self.image_features(target_img) - self.image_features(src_img)
+            edit = edit / edit.norm(dim=-1, keepdim=True)
+            loss = loss + self.lambda_direction * (1.0 - F.cosine_similarity(edit, self.target_direction)).mean()
+        if self.lambda_manifold:
+            if self.src_text_features is None:
+                s = self.get_text_features(source_class).mean(0, keepdim=True)
+                t = self.get_text_features(target_class).mean(0, keepdim=True)
+                self.src_text_features = s / s.norm(dim=-1, keepdim=True)
+                self.target_text_features = t / t.norm(dim=-1, keepdim=True)
+            cos_text = self.target_text_features @ self.src_text_features.T
+            cos_img = (self.image_features(target_img) * self.image_features(src_img)).sum(1).clamp(-1.0, 1.0)
+            loss = loss + self.lambda_manifold * (cos_img - cos_text.reshape(())).abs().mean()
+        return loss
+
+
 # ----------------------------------------------------------------------------- IR-SE50
 
 
@@ -248,13 +325,22 @@ class IDLoss(nn.Module):
 
 def compute_loss(img, original_img, styles, styles2, clip_loss, id_loss, mean, std,
                  identity_loss_coef=0.6, clip_loss_coef=1.0, l2_reg_coef=0.1,
-                 trainable=(2, 3, 5, 6, 8, 9, 11, 12), clip_loss2=None):
-    """find_direction.py:172-200; clip_loss2 = the ViT-B/16 loss of --clip_type double (:163-166: L32 + 0.5 L16)."""
+                 trainable=(2, 3, 5, 6, 8, 9, 11, 12), clip_loss2=None, clip_loss_type="default",
+                 text_prompt=None, negative_text_prompt=None):
+    """find_direction.py:172-200; clip_loss2 = the ViT-B/16 loss of --clip_type double (:163-166: L32 + 0.5 L16).
+    clip_loss_type 'nada' / 'nada_global': CLIPLossNADA objects called on the raw images with the prompts as
+    classes (:150-157)."""
     identity_loss = id_loss(img, original_img)[0] * identity_loss_coef
-    src, tgt = unprocess(original_img, mean, std), unprocess(img, mean, std)
-    clip_alignment_loss = clip_loss(src, tgt)
-    if clip_loss2 is not None:
-        clip_alignment_loss = clip_alignment_loss + 0.5 * clip_loss2(src, tgt)
+    if clip_loss_type in ("nada", "nada_global"):
+        clip_alignment_loss = clip_loss(original_img, negative_text_prompt, img, text_prompt)
+        if clip_loss2 is not None:
+            clip_alignment_loss = clip_alignment_loss + 0.5 * clip_loss2(original_img, negative_text_prompt, img,
+                                                                         text_prompt)
+    else:
+        src, tgt = unprocess(original_img, mean, std), unprocess(img, mean, std)
+        clip_alignment_loss = clip_loss(src, tgt)
+        if clip_loss2 is not None:
+            clip_alignment_loss = clip_alignment_loss + 0.5 * clip_loss2(src, tgt)
     clip_alignment_loss = clip_alignment_loss * clip_loss_coef
     t = list(trainable)
     l2 = l2_reg_coef * F.mse_loss(styles2[:, t], styles[:, t])

@@ -75,6 +75,8 @@ _SIGS = {
     "smc_face_crop_bwd_f32": (c_int, [P, c_int64] + [c_int] * 10 + [P, P]),
     "smc_clip_unprocess_f32": (c_int, [P] + [c_int] * 6 + [P, P, P, P]),
     "smc_clip_unprocess_bwd_f32": (c_int, [P, P] + [c_int] * 6 + [P, P, P, P]),
+    "smc_clip_preprocess_nada_f32": (c_int, [P] + [c_int] * 6 + [P, P, P, P]),
+    "smc_clip_preprocess_nada_bwd_f32": (c_int, [P, P] + [c_int] * 6 + [P, P, P, P]),
     "smc_linear_workspace_size": (c_int64, [c_int, c_int, c_int]),
     "smc_linear_f32": (c_int, [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P, P, c_int64, P]),
     "smc_layernorm_fwd_f32": (c_int, [P, c_int64, P, P, P, c_int64, P, P, c_int, c_int, c_float, P]),

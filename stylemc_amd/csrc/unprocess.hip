@@ -1,5 +1,9 @@
-// CLIP input preprocessing of find_direction.py:49-52 for gfx950, forward and image gradient:
+// CLIP input preprocessing for gfx950, forward and image gradient, in two forms:
+//   StyleMC (find_direction.py:49-52, MODE 0):
 //     y = (bicubic(clamp(img * 127.5 + 128, 0, 255), (out_h, out_w)) / 255 - mean[c]) / std[c]
+//   StyleGAN-NADA (clip_loss_nada.py:72-75,109-111, MODE 1): Normalize(-1, 2) -> Resize(BICUBIC) -> CenterCrop
+//   -> CLIP Normalize, no clamp:
+//     y = (bicubic((img + 1) / 2, (out_h, out_w)) - mean[c]) / std[c]
 // with the torchvision-0.8 tensor Resize (F.interpolate bicubic, align_corners=False, A = -0.75, border
 // replicate) restated from aten's upsample_bicubic2d (source index s = scale * (dst + 0.5) - 0.5, taps
 // floor(s) - 1 .. floor(s) + 2, rows interpolated first along x then along y).
@@ -23,9 +27,18 @@ __device__ __forceinline__ void cubic_coeffs(float t, float (&c)[4]) {
     c[3] = cc2(2.f - t);
 }
 
-__device__ __forceinline__ float pre(float v) {  // img * 127.5 + 128 (two roundings, as torch), clamped
-    const float x = __fadd_rn(__fmul_rn(v, 127.5f), 128.f);
-    return fminf(fmaxf(x, 0.f), 255.f);
+template <int MODE>
+__device__ __forceinline__ float pre(float v) {
+    if (MODE == 0) {  // img * 127.5 + 128 (two roundings, as torch), clamped
+        const float x = __fadd_rn(__fmul_rn(v, 127.5f), 128.f);
+        return fminf(fmaxf(x, 0.f), 255.f);
+    }
+    return __fadd_rn(v, 1.f) * 0.5f;  // torchvision Normalize(-1, 2): (v - (-1)) / 2
+}
+
+template <int MODE>
+__device__ __forceinline__ float post(float s, float mean, float std_) {
+    return MODE == 0 ? __fsub_rn(s / 255.f, mean) / std_ : __fsub_rn(s, mean) / std_;
 }
 
 struct Unproc {
@@ -35,6 +48,7 @@ struct Unproc {
     const float* std_;
 };
 
+template <int MODE>
 __global__ __launch_bounds__(256) void unprocess_fwd_kernel(const float* img, float* y, int64_t planes, Unproc q) {
     const int64_t per = (int64_t)q.out_h * q.out_w;
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -55,12 +69,12 @@ __global__ __launch_bounds__(256) void unprocess_fwd_kernel(const float* img, fl
         const float* r = p + (int64_t)yy * q.in_w;
         float v[4];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) v[b] = pre(r[min(max(ix - 1 + b, 0), q.in_w - 1)]);
+        for (int b = 0; b < 4; ++b) v[b] = pre<MODE>(r[min(max(ix - 1 + b, 0), q.in_w - 1)]);
         rows[a] = v[0] * cx[0] + v[1] * cx[1] + v[2] * cx[2] + v[3] * cx[3];
     }
     const float s = rows[0] * cy[0] + rows[1] * cy[1] + rows[2] * cy[2] + rows[3] * cy[3];
     const int c = (int)(pl % q.channels);
-    y[idx] = __fsub_rn(s / 255.f, q.mean[c]) / q.std_[c];
+    y[idx] = post<MODE>(s, q.mean[c], q.std_[c]);
 }
 
 // the (output index, tap weight) pairs of one axis that read input index i (border taps may repeat)
@@ -91,6 +105,7 @@ __device__ __forceinline__ int taps_of(int i, int in, int out, float scale, int 
     return n;
 }
 
+template <int MODE>
 __global__ __launch_bounds__(256) void unprocess_bwd_kernel(const float* img, const float* dy, float* dimg,
                                                             int64_t planes, Unproc q) {
     const int64_t per = (int64_t)q.in_h * q.in_w;
@@ -112,36 +127,71 @@ __global__ __launch_bounds__(256) void unprocess_bwd_kernel(const float* img, co
             g += r * wy[a];
         }
         const int c = (int)(pl % q.channels);
-        const float x = __fadd_rn(__fmul_rn(img[idx], 127.5f), 128.f);
-        // d/dimg of (pre(img) / 255 - mean) / std; torch.clamp passes the gradient at the bounds
-        g = (x >= 0.f && x <= 255.f) ? g / q.std_[c] / 255.f * 127.5f : 0.f;
+        if (MODE == 0) {
+            const float x = __fadd_rn(__fmul_rn(img[idx], 127.5f), 128.f);
+            // d/dimg of (pre(img) / 255 - mean) / std; torch.clamp passes the gradient at the bounds
+            g = (x >= 0.f && x <= 255.f) ? g / q.std_[c] / 255.f * 127.5f : 0.f;
+        } else {
+            g = g / q.std_[c] * 0.5f;  // d/dimg of ((img + 1) / 2 - mean) / std after the (linear) resize
+        }
     }
     dimg[idx] = g;
 }
 
 }  // namespace
 
-SMC_API int smc_clip_unprocess_f32(const float* img, int n, int channels, int in_h, int in_w, int out_h, int out_w,
-                                   const float* mean, const float* std_, float* y, void* stream) {
-    SMC_CHECK(img && y && mean && std_ && n >= 1 && channels >= 1, "smc_clip_unprocess_f32: bad args");
-    SMC_CHECK(in_h >= 1 && in_w >= 1 && out_h >= 1 && out_w >= 1, "smc_clip_unprocess_f32: bad shape");
+namespace {
+
+template <int MODE>
+int preprocess_fwd(const char* name, const float* img, int n, int channels, int in_h, int in_w, int out_h, int out_w,
+                   const float* mean, const float* std_, float* y, void* stream) {
+    SMC_CHECK(img && y && mean && std_ && n >= 1 && channels >= 1, "%s: bad args", name);
+    SMC_CHECK(in_h >= 1 && in_w >= 1 && out_h >= 1 && out_w >= 1, "%s: bad shape", name);
     const Unproc q{in_h, in_w, out_h, out_w, channels, (float)in_h / (float)out_h, (float)in_w / (float)out_w, mean,
                    std_};
     const int64_t planes = (int64_t)n * channels;
-    hipLaunchKernelGGL(unprocess_fwd_kernel, dim3((unsigned)smc::ceil_div(planes * out_h * out_w, 256)), dim3(256), 0,
-                       smc::as_stream(stream), img, y, planes, q);
-    return smc::check_launch("smc_clip_unprocess_f32");
+    hipLaunchKernelGGL(unprocess_fwd_kernel<MODE>, dim3((unsigned)smc::ceil_div(planes * out_h * out_w, 256)),
+                       dim3(256), 0, smc::as_stream(stream), img, y, planes, q);
+    return smc::check_launch(name);
+}
+
+template <int MODE>
+int preprocess_bwd(const char* name, const float* img, const float* dy, int n, int channels, int in_h, int in_w,
+                   int out_h, int out_w, const float* mean, const float* std_, float* dimg, void* stream) {
+    SMC_CHECK(img && dy && dimg && mean && std_ && n >= 1 && channels >= 1, "%s: bad args", name);
+    SMC_CHECK(in_h >= 1 && in_w >= 1 && out_h >= 1 && out_w >= 1, "%s: bad shape", name);
+    const Unproc q{in_h, in_w, out_h, out_w, channels, (float)in_h / (float)out_h, (float)in_w / (float)out_w, mean,
+                   std_};
+    const int64_t planes = (int64_t)n * channels;
+    hipLaunchKernelGGL(unprocess_bwd_kernel<MODE>, dim3((unsigned)smc::ceil_div(planes * in_h * in_w, 256)),
+                       dim3(256), 0, smc::as_stream(stream), img, dy, dimg, planes, q);
+    return smc::check_launch(name);
+}
+
+}  // namespace
+
+SMC_API int smc_clip_unprocess_f32(const float* img, int n, int channels, int in_h, int in_w, int out_h, int out_w,
+                                   const float* mean, const float* std_, float* y, void* stream) {
+    return preprocess_fwd<0>("smc_clip_unprocess_f32", img, n, channels, in_h, in_w, out_h, out_w, mean, std_, y,
+                             stream);
 }
 
 SMC_API int smc_clip_unprocess_bwd_f32(const float* img, const float* dy, int n, int channels, int in_h, int in_w,
                                        int out_h, int out_w, const float* mean, const float* std_, float* dimg,
                                        void* stream) {
-    SMC_CHECK(img && dy && dimg && mean && std_ && n >= 1 && channels >= 1, "smc_clip_unprocess_bwd_f32: bad args");
-    SMC_CHECK(in_h >= 1 && in_w >= 1 && out_h >= 1 && out_w >= 1, "smc_clip_unprocess_bwd_f32: bad shape");
-    const Unproc q{in_h, in_w, out_h, out_w, channels, (float)in_h / (float)out_h, (float)in_w / (float)out_w, mean,
-                   std_};
-    const int64_t planes = (int64_t)n * channels;
-    hipLaunchKernelGGL(unprocess_bwd_kernel, dim3((unsigned)smc::ceil_div(planes * in_h * in_w, 256)), dim3(256), 0,
-                       smc::as_stream(stream), img, dy, dimg, planes, q);
-    return smc::check_launch("smc_clip_unprocess_bwd_f32");
+    return preprocess_bwd<0>("smc_clip_unprocess_bwd_f32", img, dy, n, channels, in_h, in_w, out_h, out_w, mean,
+                             std_, dimg, stream);
+}
+
+SMC_API int smc_clip_preprocess_nada_f32(const float* img, int n, int channels, int in_h, int in_w, int out_h,
+                                         int out_w, const float* mean, const float* std_, float* y, void* stream) {
+    return preprocess_fwd<1>("smc_clip_preprocess_nada_f32", img, n, channels, in_h, in_w, out_h, out_w, mean, std_,
+                             y, stream);
+}
+
+SMC_API int smc_clip_preprocess_nada_bwd_f32(const float* img, const float* dy, int n, int channels, int in_h,
+                                             int in_w, int out_h, int out_w, const float* mean, const float* std_,
+                                             float* dimg, void* stream) {
+    return preprocess_bwd<1>("smc_clip_preprocess_nada_bwd_f32", img, dy, n, channels, in_h, in_w, out_h, out_w,
+                             mean, std_, dimg, stream);
 }

@@ -88,19 +88,26 @@ def compute_loss(img, original_img, transf, mean, std, device, clip_loss_type, c
     edited and the original image separately; DirectionFinder.step runs the batched equivalent).
 
     ``transf`` must be None: the torchvision Resize(224, BICUBIC) + CenterCrop of :258 is built into
-    ``unprocess``.  The landmarks term is 0 (computed under no_grad in the reference, :90) and the
-    StyleGAN-NADA losses are out of scope.
+    ``unprocess``.  The landmarks term is 0 (computed under no_grad in the reference, :90).  clip_loss_type
+    'nada' / 'nada_global': the loss functions are stylemc_amd.clip_loss_nada.CLIPLoss objects, called on the raw
+    images with the prompts as classes (compute_clip_loss, :150-157).
     """
     if transf is not None:
         raise ValueError("transf: the bicubic Resize + CenterCrop is built into unprocess(); pass None")
-    if clip_loss_type != "default":
-        raise NotImplementedError("the StyleGAN-NADA losses (clip_loss_nada.py) are outside the hot path")
+    if clip_loss_type not in ("default", "nada", "nada_global"):
+        raise ValueError(f"clip_loss_type must be default, nada or nada_global, got {clip_loss_type!r}")
     identity_loss = id_loss(img, original_img)[0] * identity_loss_coef
-    tgt = unprocess(img, mean, std, img_size)
-    src = unprocess(original_img, mean, std, img_size)
-    clip_alignment_loss = clip_loss1_func(src, tgt)
-    if clip_type == "double":
-        clip_alignment_loss = clip_alignment_loss + 0.5 * clip_loss2_func(src, tgt)
+    if clip_loss_type != "default":
+        clip_alignment_loss = clip_loss1_func(original_img, negative_text_prompt, img, text_prompt)
+        if clip_type == "double":
+            clip_alignment_loss = clip_alignment_loss + 0.5 * clip_loss2_func(original_img, negative_text_prompt, img,
+                                                                              text_prompt)
+    else:
+        tgt = unprocess(img, mean, std, img_size)
+        src = unprocess(original_img, mean, std, img_size)
+        clip_alignment_loss = clip_loss1_func(src, tgt)
+        if clip_type == "double":
+            clip_alignment_loss = clip_alignment_loss + 0.5 * clip_loss2_func(src, tgt)
     clip_alignment_loss = clip_loss_coef * clip_alignment_loss
     T = S_TRAINABLE_SPACE_CHANNELS
     l2 = l2_reg_coef * F.mse_loss(styles2[:, T], styles[:, T])
@@ -187,14 +194,25 @@ class DirectionFinder:
         resumed direction (none for a fresh run)."""
         return styles if self._offset is None else styles + self._offset
 
+    def _clip_inputs(self, img, orig):
+        """Per CLIP loss, its (target, source) inputs: the unprocessed 224-px images for the default loss, the raw
+        generator images for the StyleGAN-NADA losses (they preprocess themselves, clip_loss_nada.py:109-111).
+        Either image may be None (not needed by the caller)."""
+        raw = [getattr(cl, "takes_raw_images", False) for cl, _ in self.clip_losses]
+        tgt = src = None
+        if not all(raw):
+            tgt = unprocess(img, self.mean, self.std) if img is not None else None
+            with torch.no_grad():
+                src = unprocess(orig, self.mean, self.std) if orig is not None else None
+        return [(img, orig) if r else (tgt, src) for r in raw]
+
     def _original_branch(self, styles):
         """Everything that depends only on the original image (no gradient): its synthesis, its IR-SE50
         features and its CLIP embeddings."""
         with torch.no_grad():
             orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
             y_feats = self.id_loss.target_feats(orig)
-            src = unprocess(orig, self.mean, self.std)
-            src_embs = [cl.encode_src(src) for cl, _ in self.clip_losses]
+            src_embs = [cl.encode_src(s) for (cl, _), (_, s) in zip(self.clip_losses, self._clip_inputs(None, orig))]
         return y_feats, src_embs
 
     def _pair_terms(self, styles, d, key=None):
@@ -234,10 +252,8 @@ class DirectionFinder:
                 id_terms = self.id_loss.per_sample_pair(img, orig)
         else:
             id_terms = self.id_loss.per_sample_pair(img, orig)
-        tgt = unprocess(img, self.mean, self.std)
-        with torch.no_grad():
-            src = unprocess(orig, self.mean, self.std)
-        clip_terms = sum(w * cl.per_sample_pair(tgt, src) for cl, w in self.clip_losses)
+        clip_terms = sum(w * cl.per_sample_pair(t, s) for (cl, w), (t, s) in zip(self.clip_losses,
+                                                                                  self._clip_inputs(img, orig)))
         if side is not None:
             main.wait_stream(side)
             id_terms.record_stream(main)
@@ -268,8 +284,8 @@ class DirectionFinder:
             img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
             y_feats, src_embs = self._original_branch(styles)
         id_terms = self.id_loss.per_sample_with(img, y_feats)
-        tgt = unprocess(img, self.mean, self.std)
-        clip_terms = sum(w * cl.per_sample_with(e, tgt) for (cl, w), e in zip(self.clip_losses, src_embs))
+        clip_terms = sum(w * cl.per_sample_with(e, t) for (cl, w), e, (t, _) in
+                         zip(self.clip_losses, src_embs, self._clip_inputs(img, None)))
         return self._finish(styles, d, id_terms, clip_terms, denom)
 
     def _finish(self, styles, d, id_terms, clip_terms, denom):
@@ -410,11 +426,16 @@ def load_text_features(path):
 
 def build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip_loss_type="default", impl="hip",
                       clip_weights=None, text_features=None, bpe_path=None, synthetic_weights=False):
-    """init_clip_loss (find_direction.py:100-122) for the default loss: [(CLIPLoss, weight)], 'double' ->
-    ViT-B/32 at 1 + ViT-B/16 at 0.5 (:163-166).  clip_weights / text_features: {'small'|'large': ...}."""
+    """init_clip_loss (find_direction.py:100-122): [(loss, weight)], 'double' -> ViT-B/32 at 1 + ViT-B/16 at 0.5
+    (:155,163-166).  clip_loss_type 'default' -> clip_loss.CLIPLoss; 'nada' -> clip_loss_nada.CLIPLoss with the
+    directional term, 'nada_global' -> with the global term only (:100-114), each bound to (negative prompt,
+    prompt) as (source, target) class (:150-157).  clip_weights / text_features: {'small'|'large': ...}."""
     from .clip_loss import MODEL_NAMES, CLIPLoss
-    if clip_loss_type != "default":
-        raise NotImplementedError("the StyleGAN-NADA losses (clip_loss_nada.py) are outside the hot path")
+    if clip_loss_type not in ("default", "nada", "nada_global"):
+        raise ValueError(f"--clip_loss_type must be default, nada or nada_global, got {clip_loss_type!r}")
+    if clip_loss_type != "default" and any(v is not None for v in (text_features or {}).values()):
+        raise ValueError("--text_features holds the default loss' prompt direction; the NADA losses encode the "
+                         "templated prompts themselves (CLIP weights with the text tower + --clip_bpe)")
     kinds = [("small", 1.0), ("large", 0.5)] if clip_type == "double" else [(clip_type, 1.0)]
     clip_weights = {k: v for k, v in (clip_weights or {}).items() if v}
     text_features = {k: v for k, v in (text_features or {}).items() if v is not None}
@@ -426,6 +447,16 @@ def build_clip_losses(clip_type, device, text_prompt, negative_text_prompt, clip
                              f"(--clip_weights for ViT-B/32, --clip_weights_large for ViT-B/16)")
         synthetic_weights = False
     out = []
+    if clip_loss_type != "default":
+        from . import clip_loss_nada
+        lam = dict(lambda_direction=0.0, lambda_global=1.0) if clip_loss_type == "nada_global" else {}
+        for kind, w in kinds:
+            path = clip_weights.get(kind)
+            loss = clip_loss_nada.CLIPLoss(device, clip_model=MODEL_NAMES[kind], impl=impl, bpe_path=bpe_path,
+                                           clip_state_dict=_load_weights(path) if path else None,
+                                           synthetic_weights=synthetic_weights, **lam)
+            out.append((clip_loss_nada.NadaTerms(loss, negative_text_prompt, text_prompt), w))
+        return out
     for kind, w in kinds:
         path = clip_weights.get(kind)
         out.append((CLIPLoss(device, text_prompt, negative_text_prompt, kind, impl=impl,

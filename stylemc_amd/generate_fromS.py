@@ -14,7 +14,10 @@ Restates generate_fromS.py:58-209:
 New (README.md:54-56 names a video flag the reference never implemented): ``--from_video N`` renders
 N frames per item with power linspace(0, change_power, N) (no in-place drift: styles[i] + d*p), batched
 on the GPU, written as JPEG frames + one uint8 .npy stack per item.
-Out of scope: deeplab feature blending (--use_blending) and a second generator (--network2).
+--network2 (:42-43,80-86,168-170): the edited image (j = 1, power change_power) is rendered by a second generator
+G2 with its own temp shapes; the original (power 0) by G.  In the video sweep, power-0 frames come from G and
+every other frame from G2.
+Out of scope: deeplab feature blending (--use_blending).
 """
 import os
 import time
@@ -55,32 +58,43 @@ def render_projected_w(G, ws, noise_mode="const"):
 
 @torch.no_grad()
 def render_pairs(G, styles, direction, change_power, temp_shapes, noise_mode="const", until_k=100, mapper=None,
-                 use_whitelist=False):
+                 use_whitelist=False, G2=None, temp_shapes2=None):
     """Yield (i, [orig_uint8, edited_uint8]) replaying the reference's in-place styles drift.  direction is
-    the global [1, 26, 512] direction, or None with a ``mapper`` (per-item direction)."""
+    the global [1, 26, 512] direction, or None with a ``mapper`` (per-item direction).  G2 (--network2): the
+    generator of the edited image (generate_fromS.py:168-170)."""
     for i in range(styles.shape[0]):
         imgs = []
-        for p in [0, change_power]:
+        for j, p in enumerate([0, change_power]):
             if mapper is not None:
                 direction = mapper_direction(mapper, styles[i], use_whitelist)
             styles += direction * p
-            _, img = utils.generate_image(G, until_k, styles[[i]], temp_shapes, noise_mode)
+            g, ts = (G2, temp_shapes2) if (G2 is not None and j == 1) else (G, temp_shapes)
+            _, img = utils.generate_image(g, until_k, styles[[i]], ts, noise_mode)
             imgs.append(to_uint8(img)[0])
             styles -= direction * p
         yield i, imgs
 
 
 @torch.no_grad()
-def render_sweep(G, style_row, direction, powers, temp_shapes, noise_mode="const", batch=8, until_k=100):
-    """Frames for one S row along the direction: uint8 [len(powers), H, W, 3]."""
-    out = []
-    powers = torch.as_tensor(powers, dtype=torch.float32, device=style_row.device)
-    for lo in range(0, len(powers), batch):
-        p = powers[lo:lo + batch].view(-1, 1, 1)
-        s = style_row.unsqueeze(0) + direction * p
-        _, img = utils.generate_image(G, until_k, s, temp_shapes, noise_mode)
-        out.append(to_uint8(img))
-    return torch.cat(out)
+def render_sweep(G, style_row, direction, powers, temp_shapes, noise_mode="const", batch=8, until_k=100, G2=None,
+                 temp_shapes2=None):
+    """Frames for one S row along the direction: uint8 [len(powers), H, W, 3].  G2: renders every frame whose
+    power is not 0 (the edited frames; --network2)."""
+    powers = [float(p) for p in np.asarray(powers, dtype=np.float64)]
+    groups = [(G, temp_shapes, [k for k, p in enumerate(powers) if G2 is None or p == 0.0])]
+    if G2 is not None:
+        groups.append((G2, temp_shapes2, [k for k, p in enumerate(powers) if p != 0.0]))
+    out = [None] * len(powers)
+    pw = torch.as_tensor(powers, dtype=torch.float32, device=style_row.device)
+    for g, ts, ks in groups:
+        for lo in range(0, len(ks), batch):
+            idx = ks[lo:lo + batch]
+            p = pw[torch.as_tensor(idx, device=style_row.device)].view(-1, 1, 1)
+            s = style_row.unsqueeze(0) + direction * p
+            _, img = utils.generate_image(g, until_k, s, ts, noise_mode)
+            for k, fr in zip(idx, to_uint8(img)):
+                out[k] = fr
+    return torch.stack(out)
 
 
 def _cli():
@@ -89,7 +103,8 @@ def _cli():
     @click.command()
     @click.option("--network", "network_pkl", default="synthetic",
                   help="network pickle / G_ema state_dict, or 'synthetic'")
-    @click.option("--network2", "network2_pkl", default=None, help="(unsupported: second generator)")
+    @click.option("--network2", "network2_pkl", default=None,
+                  help="second generator for the edited image (default: --network)")
     @click.option("--noise-mode", type=click.Choice(["const", "random", "none"]), default="const", show_default=True)
     @click.option("--projected-w", "projected_w", type=str, default=None, metavar="FILE",
                   help="npz with key 'w' [n, num_ws, 512]: render each W with G.synthesis")
@@ -112,10 +127,15 @@ def _cli():
         from PIL import Image
 
         from .find_direction import load_generator
-        if use_blending or (network2_pkl and network2_pkl != network_pkl):
-            raise SystemExit("deeplab blending / second-generator paths are outside the hot path")
+        if use_blending:
+            raise SystemExit("deeplab feature blending (--use_blending) is outside the hot path")
         device = torch.device("cuda")
         G = load_generator(network_pkl, resolution, device, conv_clamp=conv_clamp)
+        G2 = temp_shapes2 = None
+        if network2_pkl and network2_pkl != network_pkl:
+            print("using 2 generators")
+            G2 = load_generator(network2_pkl, resolution, device, conv_clamp=conv_clamp)
+            temp_shapes2 = utils.get_temp_shapes(G2)
         os.makedirs(outdir, exist_ok=True)
         stem = text_prompt.replace(" ", "_")
         if projected_w is not None:
@@ -142,7 +162,8 @@ def _cli():
             powers = np.linspace(0.0, change_power, from_video)
             for i in range(styles.shape[0]):
                 d = mapper_direction(mapper, styles[i], use_whitelist) if mapper is not None else direction
-                frames = render_sweep(G, styles[i], d, powers, temp_shapes, noise_mode, video_batch)
+                frames = render_sweep(G, styles[i], d, powers, temp_shapes, noise_mode, video_batch, G2=G2,
+                                      temp_shapes2=temp_shapes2)
                 arr = frames.cpu().numpy()
                 base = f"{outdir}/{stem}_{i:03d}"
                 np.save(base + "_frames.npy", arr)
@@ -150,7 +171,7 @@ def _cli():
                     Image.fromarray(fr, "RGB").save(f"{base}_f{k:03d}.jpeg", quality=95)
         else:
             for i, imgs in render_pairs(G, styles, direction, change_power, temp_shapes, noise_mode, mapper=mapper,
-                                        use_whitelist=bool(use_whitelist)):
+                                        use_whitelist=bool(use_whitelist), G2=G2, temp_shapes2=temp_shapes2):
                 arr = np.concatenate([im.cpu().numpy() for im in imgs], axis=1)
                 Image.fromarray(arr, "RGB").save(f"{outdir}/{stem}_{i:03d}.jpeg", quality=95)
         print("time passed:", time.time() - t1)

@@ -157,3 +157,9 @@ def text_direction(text_prompt, negative_text_prompt, dim=512, seed=0):
     key = f"{text_prompt}\x00{negative_text_prompt}"
     t = _normal((1, dim), seed, "text:" + key)
     return t / t.norm(dim=1, keepdim=True)
+
+
+def text_embeddings(strings, dim=512, seed=0):
+    """Seeded stand-in for E_T(tokenize(s)) per string (un-normalised, [len(strings), dim]) when no CLIP text
+    weights exist: the StyleGAN-NADA losses encode 27 templated prompts per class (clip_loss_nada.py:126-136)."""
+    return torch.stack([_normal((dim,), seed, "textemb:" + s) for s in strings])

@@ -500,6 +500,134 @@ def gen_losses():
     save("loss_composition.npz", out)
 
 
+class _Tok:
+    """What the stubbed ``clip.tokenize`` returns: the strings themselves (E_T is a seeded per-string stand-in)."""
+
+    def __init__(self, strings):
+        self.strings = list(strings)
+
+    def to(self, device):
+        return self
+
+
+class _NadaClipModel:
+    """Stands in for the model ``clip.load`` returns to clip_loss_nada.CLIPLoss: encode_image = the seeded oracle
+    ViT, encode_text = synthetic.text_embeddings (seeded E_T per string), and the openai/CLIP ``CLIP.forward``
+    (normalise both, logit_scale.exp() * cos) restated for the global loss (third-party: parity unpinned)."""
+
+    def __init__(self, visual, logit_scale):
+        self.visual = visual
+        self.logit_scale = torch.tensor(logit_scale, dtype=torch.float32)
+
+    def encode_image(self, image):
+        return self.visual(image)
+
+    def encode_text(self, tokens):
+        return synthetic.text_embeddings(tokens.strings)
+
+    def __call__(self, image, tokens):
+        i = self.encode_image(image)
+        t = self.encode_text(tokens)
+        i = i / i.norm(dim=1, keepdim=True)
+        t = t / t.norm(dim=1, keepdim=True)
+        logits = self.logit_scale.exp() * i @ t.t()
+        return logits, logits.t()
+
+
+def import_reference_nada():
+    """The reference clip_loss_nada module with import-only stubs (clip, torchvision.transforms); must be imported
+    before import_reference_losses() replaces it by a stub."""
+    stub = sys.modules.get("clip_loss_nada")
+    if stub is not None and getattr(stub, "__file__", None) is None:
+        del sys.modules["clip_loss_nada"]
+    clip = _stub("clip", load=_Absent, tokenize=_Absent)
+    clip.tokenize = lambda strings: _Tok([strings] if isinstance(strings, str) else strings)
+    tv = _stub("torchvision")
+    tv.transforms = _stub("torchvision.transforms", Compose=_Absent, Resize=_Absent, CenterCrop=_Absent,
+                          Normalize=_Absent)
+    import clip_loss_nada as ref_nada                          # clip_loss_nada.py
+    return ref_nada
+
+
+def nada_preprocess_transf(x):
+    """clip_loss_nada.py:72-75 preprocess: torchvision Normalize(-1, 2) (sub_ then div_), the CLIP preprocess'
+    Resize(224, BICUBIC) + CenterCrop(224) (bicubic_transf), CLIP Normalize -- restated (torchvision / clip absent)."""
+    mean, std = ref_utils.get_mean_std("cpu")
+    return (bicubic_transf((x - (-1.0)) / 2.0) - mean) / std
+
+
+def ref_nada_obj(ref_nada, visual, lambda_direction=1.0, lambda_global=0.0, lambda_manifold=0.0):
+    """The reference clip_loss_nada.CLIPLoss (:62-101) without clip.load: model / preprocess / losses set."""
+    import math
+    obj = ref_nada.CLIPLoss.__new__(ref_nada.CLIPLoss)
+    torch.nn.Module.__init__(obj)
+    obj.device = "cpu"
+    obj.model = _NadaClipModel(visual, math.log(100.0))
+    obj.clip_preprocess = None
+    obj.preprocess = nada_preprocess_transf
+    obj.target_direction = None
+    obj.patch_text_directions = None
+    obj.patch_loss = ref_nada.DirectionLoss("mae")
+    obj.direction_loss = ref_nada.DirectionLoss("cosine")
+    obj.patch_direction_loss = torch.nn.CosineSimilarity(dim=2)
+    obj.lambda_global, obj.lambda_patch, obj.lambda_direction = lambda_global, 0.0, lambda_direction
+    obj.lambda_manifold, obj.lambda_texture = lambda_manifold, 0.0
+    obj.src_text_features = None
+    obj.target_text_features = None
+    obj.angle_loss = torch.nn.L1Loss()
+    return obj
+
+
+NADA_CASES = {"nada": dict(lambda_direction=1.0), "nada_global": dict(lambda_direction=0.0, lambda_global=1.0),
+              "mix": dict(lambda_direction=1.0, lambda_global=0.5, lambda_manifold=0.7)}
+
+
+def gen_nada():
+    """clip_loss_nada.CLIPLoss.forward of the REFERENCE (clip_loss_nada.py:117-229,324-346: template text direction,
+    directional / global / angle losses) on seeded 512-px images, and find_direction.compute_loss with
+    --clip_loss_type nada / nada_global, clip_type small and double (find_direction.py:100-114,150-157,172-200)."""
+    ref_nada = import_reference_nada()
+    ref_fd, ref_cl, ref_il = import_reference_losses()
+    T = ref_fd.S_TRAINABLE_SPACE_CHANNELS
+    out = {}
+    src_class, tgt_class = LOSS_TEXT[1], LOSS_TEXT[0]
+    for case, kw in NADA_CASES.items():
+        obj = ref_nada_obj(ref_nada, seeded_visual("ViT-B/32", 4), **kw)
+        img, orig, _, _ = loss_inputs()
+        img.requires_grad_(True)
+        loss = obj(orig, src_class, img, tgt_class)
+        (dimg,) = torch.autograd.grad(loss, img)
+        p = f"forward/{case}/"
+        out[p + "loss"] = loss.detach()
+        out[p + "dimg_blocks8"] = block_sums(dimg, 8).float()
+        out[p + "dimg_probes"] = probes(dimg)
+        if obj.target_direction is not None:
+            out[p + "target_direction"] = obj.target_direction
+    out["preprocess_img"] = nada_preprocess_transf(loss_inputs()[0])[:, :, ::8, ::8]
+    idl = ref_id_loss_obj(ref_il)
+    mean, std = ref_utils.get_mean_std("cpu")
+    for clip_loss_type in ("nada", "nada_global"):
+        kw = NADA_CASES[clip_loss_type]
+        for clip_type in ("small", "double"):
+            cl1 = ref_nada_obj(ref_nada, seeded_visual("ViT-B/32", 4), **kw)
+            cl2 = ref_nada_obj(ref_nada, seeded_visual("ViT-B/16", 4), **kw) if clip_type == "double" else None
+            img, orig, styles, delta = loss_inputs()
+            img.requires_grad_(True)
+            sdir = torch.zeros(1, 26, 512)
+            sdir[:, T] = delta
+            loss, parts = ref_fd.compute_loss(
+                img, orig, bicubic_transf, mean, std, "cpu", clip_loss_type, clip_type, 1.0, cl1, cl2, LOSS_TEXT[0],
+                LOSS_TEXT[1], idl, 0.6, None, 0.0, None, 224, styles, styles + sdir, 0.1)
+            (dimg,) = torch.autograd.grad(loss, img)
+            p = f"{clip_loss_type}/{clip_type}/"
+            out[p + "loss"] = loss.detach()
+            for k in ("clip_loss", "identity_loss", "l2_loss"):
+                out[p + k] = torch.as_tensor(parts[k]).detach()
+            out[p + "dimg_blocks8"] = block_sums(dimg, 8).float()
+            out[p + "dimg_probes"] = probes(dimg)
+    save("loss_nada.npz", out)
+
+
 def gen_styles():
     """utils.split_ws / utils.get_styles of the REFERENCE (utils.py:77-87,123-158) on a small generator (b4 must
     be 512 wide: utils.py:135 writes the b4 row at full width)."""
@@ -594,7 +722,7 @@ def gen_config1():
 
 if __name__ == "__main__":
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    which = sys.argv[1:] or ["upfirdn2d", "bias_act", "conv2d_resample", "synthesis", "irse50", "clip", "losses",
-                             "styles", "config1"]
+    which = sys.argv[1:] or ["upfirdn2d", "bias_act", "conv2d_resample", "synthesis", "irse50", "clip", "nada",
+                             "losses", "styles", "config1"]
     for w in which:
         globals()[f"gen_{w}"]()

@@ -104,3 +104,62 @@ def test_generate_fromS_projected_w_vs_oracle():
     ref = OG.render_projected_w(Go, ws.cpu())
     for a, b in zip(got, ref):
         _check_u8(a, b, "projected w")
+
+
+def test_generate_fromS_config5_video_sweep_64_frames():
+    """BASELINE config 5: the FFHQ-1024 --from_video sweep, change_power 0 -> 50, 64 frames rendered on the GPU in
+    batches of 8; frames {0, 21, 42, 63} checked per pixel against the oracle (the uint8 tolerance above)."""
+    from stylemc_amd import generate_fromS, utils
+    G, Go = _pair(1024, 32768)
+    style_row = synthetic.synthetic_styles(1, seed=3)[0]
+    direction = torch.zeros(1, 26, 512)
+    direction[:, utils.S_TRAINABLE_SPACE_CHANNELS] = torch.randn(1, 8, 512, generator=torch.Generator().manual_seed(2)) * 0.1
+    powers = np.linspace(0.0, 50.0, 64)
+    got = generate_fromS.render_sweep(G, style_row.to(DEV), direction.to(DEV), powers, utils.get_temp_shapes(G),
+                                      batch=8)
+    assert got.shape == (64, 1024, 1024, 3)
+    idx = [0, 21, 42, 63]
+    ref = OG.render_sweep(Go, style_row, direction, powers[idx], OS.get_temp_shapes(Go))
+    _check_u8(got[idx], ref, "config 5 sweep")
+    # the frames differ along the sweep (the direction is applied)
+    assert (got[0].int() - got[63].int()).abs().float().mean() > 1.0
+
+
+def _second_generator(res, cbase, seed):
+    from stylemc_amd import networks
+    cfg = synthetic.generator_config(resolution=res, channel_base=cbase)
+    sd = synthetic.generator_state_dict(cfg, seed=seed)
+    G2 = networks.build_generator(cfg, sd, device=DEV)
+    Go2 = ON.Generator(512, 0, 512, res, 3, channel_base=cbase, conv_clamp=cfg["conv_clamp"])
+    Go2.load_state_dict(sd, strict=False)
+    return G2, Go2.eval().requires_grad_(False)
+
+
+@pytest.mark.parametrize("res,cbase", [(32, 512), (256, 16384)])
+def test_generate_fromS_network2_vs_oracle(res, cbase):
+    """--network2 (generate_fromS.py:80-86,168-170): the edited image from a second seeded generator, the original
+    from the first; per-pixel vs the oracle, and the edited image differs from G's own rendering."""
+    from stylemc_amd import generate_fromS, utils
+    G, Go = _pair(res, cbase)
+    G2, Go2 = _second_generator(res, cbase, seed=1)
+    styles = synthetic.synthetic_styles(2, seed=9)
+    direction = torch.zeros(1, 26, 512)
+    direction[:, utils.S_TRAINABLE_SPACE_CHANNELS] = torch.randn(1, 8, 512, generator=torch.Generator().manual_seed(1)) * 0.3
+    ts, ts2 = utils.get_temp_shapes(G), utils.get_temp_shapes(G2)   # (get_temp_shapes replaces the affines)
+    tso, tso2 = OS.get_temp_shapes(Go), OS.get_temp_shapes(Go2)
+    got = list(generate_fromS.render_pairs(G, styles.to(DEV), direction.to(DEV), 2.0, ts, G2=G2, temp_shapes2=ts2))
+    ref = OG.render_pairs(Go, styles.clone(), direction, 2.0, tso, G2=Go2, temp_shapes2=tso2)
+    one = list(generate_fromS.render_pairs(G, styles.to(DEV), direction.to(DEV), 2.0, ts))
+    for (i, imgs), rimgs, (_, single) in zip(got, ref, one):
+        for k in range(2):
+            _check_u8(imgs[k], rimgs[k], f"item {i} power {k}")
+        assert torch.equal(imgs[0], single[0])
+        assert not torch.equal(imgs[1], single[1])
+    # video sweep: power-0 frames from G, the rest from G2
+    powers = [0.0, 1.0, 2.0]
+    frames = generate_fromS.render_sweep(G, styles[0].to(DEV), direction.to(DEV), powers, ts, batch=2, G2=G2,
+                                         temp_shapes2=ts2)
+    ref0 = OG.render_sweep(Go, styles[0], direction, powers[:1], tso)
+    ref12 = OG.render_sweep(Go2, styles[0], direction, powers[1:], tso2)
+    _check_u8(frames[:1], ref0, "sweep G frame")
+    _check_u8(frames[1:], ref12, "sweep G2 frames")
