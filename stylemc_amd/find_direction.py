@@ -132,8 +132,10 @@ class DirectionFinder:
     def __init__(self, G, styles_array, clip_losses, id_loss, resolution=1024, batch_size=4, learning_rate=1.5,
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
-                 overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None):
+                 overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None, G2=None, temp_shapes2=None):
         self.G = G
+        # the edited image's generator (train_latent_mapper.py:100-106,159-162 --network2; default G itself)
+        self.G_edit = G2 if G2 is not None else G
         # how the side / prefetch streams are made (default: torch's stream pool); tools/stream_ab.py A/Bs it
         self.stream_factory = stream_factory or (lambda dev: torch.cuda.Stream(device=dev))
         self.synth_fn = synth_fn or utils.generate_image_rows   # (G, until_k, styles, shapes, noise, delta=)
@@ -159,6 +161,8 @@ class DirectionFinder:
         self.noise_mode = noise_mode
         self.world = world or _dist.World()
         self.temp_shapes = temp_shapes if temp_shapes is not None else utils.get_temp_shapes(G)
+        self.temp_shapes_edit = self.temp_shapes if G2 is None else (
+            temp_shapes2 if temp_shapes2 is not None else utils.get_temp_shapes(G2))
         self.n_items = styles_array.shape[0]
         self.num_batches = math.ceil(self.n_items / self.B)
         self.total_iterations = self.num_batches * n_epochs
@@ -206,6 +210,12 @@ class DirectionFinder:
                 src = unprocess(orig, self.mean, self.std) if orig is not None else None
         return [(img, orig) if r else (tgt, src) for r in raw]
 
+    def _synth_edited(self, styles, d):
+        """The edited image: styles (+ a resumed direction's fixed rows) with ``d`` on the trainable rows -- d is
+        [1, 8, 512] (find_direction) or [n, 8, 512] (the latent mapper's per-sample delta)."""
+        return self.synth_fn(self.G_edit, self.until_k, self._edited(styles), self.temp_shapes_edit, self.noise_mode,
+                             delta=d)
+
     def _original_branch(self, styles):
         """Everything that depends only on the original image (no gradient): its synthesis, its IR-SE50
         features and its CLIP embeddings."""
@@ -223,7 +233,7 @@ class DirectionFinder:
         pref, self._pref = self._pref, None
         if side is not None and pref is not None and pref[0] == key:
             main = torch.cuda.current_stream()
-            img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
+            img = self._synth_edited(styles, d)
             main.wait_stream(self._pre)
             orig = pref[1]
             orig.record_stream(main)
@@ -232,11 +242,11 @@ class DirectionFinder:
             side.wait_stream(main)
             with torch.cuda.stream(side), torch.no_grad():
                 orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
-            img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
+            img = self._synth_edited(styles, d)
             main.wait_stream(side)
             orig.record_stream(main)
         else:
-            img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
+            img = self._synth_edited(styles, d)
             with torch.no_grad():
                 orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
         if side is not None:
@@ -259,14 +269,15 @@ class DirectionFinder:
             id_terms.record_stream(main)
         return id_terms, clip_terms
 
-    def _local_terms(self, styles, denom, key=None):
-        """Sum-form loss of this rank's shard: every per-sample term / global batch size.
+    def _local_terms(self, styles, denom, key=None, d=None):
+        """Sum-form loss of this rank's shard: every per-sample term / global batch size.  Returns the gradient
+        w.r.t. ``d`` (default: a leaf copy of the shared direction) and the 4 loss terms.
 
         On the GPU the original-image branch runs on a second HIP stream, concurrently with the edited
         image's synthesis (it shares no data with it), and joins before the losses.
         """
-        T = S_TRAINABLE_SPACE_CHANNELS
-        d = self.delta.detach().clone().requires_grad_(True)
+        if d is None:
+            d = self.delta.detach().clone().requires_grad_(True)
         if self.batch_losses:
             id_terms, clip_terms = self._pair_terms(styles, d, key)
             return self._finish(styles, d, id_terms, clip_terms, denom)
@@ -276,12 +287,12 @@ class DirectionFinder:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 y_feats, src_embs = self._original_branch(styles)
-            img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
+            img = self._synth_edited(styles, d)
             main.wait_stream(side)
             for t in [y_feats] + src_embs:
                 t.record_stream(main)
         else:
-            img = self.synth_fn(self.G, self.until_k, self._edited(styles), self.temp_shapes, self.noise_mode, delta=d)
+            img = self._synth_edited(styles, d)
             y_feats, src_embs = self._original_branch(styles)
         id_terms = self.id_loss.per_sample_with(img, y_feats)
         clip_terms = sum(w * cl.per_sample_with(e, t) for (cl, w), e, (t, _) in

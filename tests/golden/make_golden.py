@@ -720,9 +720,90 @@ def gen_config1():
                                    "meta": np.array([resolution, batch_size, n_epochs, seed])})
 
 
+MAPPER_SUBSAMPLE = 61   # every 61st parameter element is stored (the mapper has 5.3 M parameters)
+
+
+def flat_params(module):
+    return torch.cat([p.detach().reshape(-1) for p in module.parameters()])
+
+
+def gen_mapper_train():
+    """The REFERENCE's train_latent_mapper loop (train_latent_mapper.py:138-196, statement for statement; click /
+    wandb / landmark plumbing left out) on BASELINE config 1's problem (paper256 FFHQ-256, S codes of seeds 1-4),
+    batch 2, 2 epochs (4 iterations), the script's defaults (lr 0.0005, identity 0.3, l2 0.8, clip 2.0, clip_type
+    small), driven by the reference's Mapper, generate_image and compute_loss and torch Adam, from a seeded mapper
+    passed the way --resume passes one (:118-120).  Stored: the per-iteration log, and the parameter update and the
+    first iteration's gradient as per-tensor norms + every MAPPER_SUBSAMPLE-th element."""
+    import math
+    tv = _stub("torchvision")
+    tv.transforms = _stub("torchvision.transforms", Compose=_Absent, Resize=_Absent, CenterCrop=_Absent)
+    _stub("encoder4editing.models.stylegan2.op", FusedLeakyReLU=_Absent, fused_leaky_relu=_Absent, upfirdn2d=_Absent)
+    import latent_mappers as ref_lm
+    ref_fd, ref_cl, ref_il = import_reference_losses()
+    T = ref_fd.S_TRAINABLE_SPACE_CHANNELS
+    cfg, sd, ws = config1_problem()
+    G = RefG(cfg).eval()
+    G.load_state_dict({k: v for k, v in sd.items() if k.startswith("synthesis.")}, strict=False)
+    G.synthesis.w_dim = 512
+    G.synthesis.num_ws = ws.shape[1]
+    G.requires_grad_(False)
+    styles_array, temp_shapes = ref_utils.get_styles(G, ws, ref_utils.split_ws(G, ws), "cpu")
+    mean, std = ref_utils.get_mean_std("cpu")
+    idl = ref_id_loss_obj(ref_il)
+    cl = ref_clip_loss_obj(ref_cl, seeded_visual("ViT-B/32", 4), synthetic.text_direction(*LOSS_TEXT))
+    resolution, batch_size, learning_rate, n_epochs, seed, neg_slope = 256, 2, 0.0005, 2, 3, 0.01
+    mapper = ref_lm.Mapper(neg_slope)
+    mapper.load_state_dict(synthetic.seeded_state_dict(mapper, seed=8))
+    start = flat_params(mapper).clone()
+    opt = torch.optim.Adam(mapper.parameters(), lr=learning_rate, betas=(0.9, 0.999))
+    n_items = styles_array.size(0)
+    num_batches = math.ceil(n_items / batch_size)
+    total = num_batches * n_epochs
+    np.random.seed(seed)
+    it = 0
+    log, grad0 = [], None
+    for _ in range(n_epochs):
+        for _ in range(num_batches):
+            opt.zero_grad()
+            it += 1
+            lr = np.cos(np.pi * it / total) * learning_rate * 0.5 + learning_rate * 0.5
+            for group in opt.param_groups:
+                group["lr"] = lr
+            i = np.random.randint(0, math.ceil(n_items / batch_size))
+            styles = styles_array[i * batch_size:(i + 1) * batch_size]
+            delta = mapper(styles[:, T, :])
+            styles2 = styles.clone()
+            styles2[:, T] += delta
+            _, img = ref_utils.generate_image(G, {256: 6, 512: 7, 1024: 8}[resolution], styles2, temp_shapes, "const",
+                                              "cpu")
+            _, original_img = ref_utils.generate_image(G, {256: 6, 512: 7, 1024: 8}[resolution], styles, temp_shapes,
+                                                       "const", "cpu")
+            loss, parts = ref_fd.compute_loss(
+                img, original_img, bicubic_transf, mean, std, "cpu", "default", "small", 2.0, cl, None,
+                LOSS_TEXT[0], LOSS_TEXT[1], idl, 0.3, None, 0.0, None, 224, styles, styles2, 0.8)
+            loss.backward(retain_graph=True)
+            grad_norm = sum(p.grad.data.norm() for p in mapper.parameters() if p.grad is not None)
+            if grad0 is None:
+                grad0 = torch.cat([p.grad.detach().reshape(-1) for p in mapper.parameters()])
+            opt.step()
+            log.append([it, i, lr, float(loss), float(parts["clip_loss"]), float(parts["identity_loss"]),
+                        float(parts["l2_loss"]), float(grad_norm)])
+            print(log[-1])
+    update = flat_params(mapper) - start
+    sizes = np.array([p.numel() for p in mapper.parameters()])
+    bounds = np.concatenate([[0], np.cumsum(sizes)])
+    save("mapper_train.npz", {
+        "log": np.array(log), "meta": np.array([resolution, batch_size, n_epochs, seed]),
+        "meta_f": np.array([learning_rate, neg_slope]), "styles": styles_array,
+        "update_sub": update[::MAPPER_SUBSAMPLE], "grad0_sub": grad0[::MAPPER_SUBSAMPLE],
+        "update_norms": np.array([update[a:b].norm().item() for a, b in zip(bounds[:-1], bounds[1:])]),
+        "grad0_norms": np.array([grad0[a:b].norm().item() for a, b in zip(bounds[:-1], bounds[1:])]),
+        "param_names": np.array([n for n, _ in mapper.named_parameters()])})
+
+
 if __name__ == "__main__":
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     which = sys.argv[1:] or ["upfirdn2d", "bias_act", "conv2d_resample", "synthesis", "irse50", "clip", "nada",
-                             "losses", "styles", "config1"]
+                             "losses", "styles", "config1", "mapper_train"]
     for w in which:
         globals()[f"gen_{w}"]()
