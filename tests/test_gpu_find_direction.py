@@ -86,14 +86,15 @@ def test_find_direction_ffhq1024_bs4_vs_oracle():
 
 
 def test_find_direction_ffhq1024_bs8_vs_oracle():
-    """BASELINE config 4 with the real batch: find_direction --batch_size 8 (16 images per loss network)."""
-    _check(*_run_pair(1024, 32768, n_items=8, bs=8, iters=1), max_err=1e-2)
+    """BASELINE config 4 with the real batch: find_direction --batch_size 8 (16 images per loss network), two
+    iterations over 8 S codes (the second step runs on the SGD-updated direction)."""
+    _check(*_run_pair(1024, 32768, n_items=8, bs=8, iters=2), max_err=1e-2)
 
 
 def test_find_direction_ffhq1024_torch_losses_vs_oracle():
-    """BASELINE config 2: CLIP ViT-B/32 and IR-SE50 on PyTorch-ROCm ops (--clip-impl/--id-impl torch), the
-    synthesis on the HIP kernels, forward and backward through the whole loop."""
-    _check(*_run_pair(1024, 32768, n_items=3, bs=2, iters=2, impl="torch"), max_err=1e-2)
+    """BASELINE config 2 at its stated batch: FFHQ-1024, batch 4, CLIP ViT-B/32 and IR-SE50 on PyTorch-ROCm ops
+    (--impl torch), the synthesis on the HIP kernels, forward and backward through two iterations."""
+    _check(*_run_pair(1024, 32768, n_items=4, bs=4, iters=2, impl="torch"), max_err=1e-2)
 
 
 def test_first_step_overlap_matches_serial():
