@@ -214,14 +214,19 @@ def dist_selfcheck(G, clip, id_loss, world, dev, temp_shapes, resolution, batch,
 
 
 def pmc_traffic():
+    """(bytes per conv-family launch, where the number comes from): PMC counters need their own rocprofv3 passes
+    (tools/pmc_bench.sh), so the bench line carries the last recorded passes' figure and says which."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as f:
-            return json.load(f).get("conv_gemm_bytes_per_launch")
+            d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
+    src = (f"profiles/pmc_traffic.json ({d.get('recorded', 'r02 v13')}): {d.get('method', 'rocprofv3 PMC passes')}; "
+           f"not measured in this run")
+    return d.get("conv_gemm_bytes_per_launch"), src
 
 
 def main():
@@ -303,15 +308,26 @@ def main():
             "direct": ("direct implicit-GEMM kernels (conv_gemm_lds / conv_row / convt_lds ...: transposed conv0, "
                        "its stride-2 data grad, the < 32-px layers); FLOPs = dense MACs x 2"),
         }
+        traffic, traffic_src = pmc_traffic()
+        parts = {k: part(s["kinds"][k], kinds.get(k, k)) for k in sorted(s["kinds"])}
+        dom = max(parts, key=lambda k: parts[k]["ms_per_step"]) if parts else None
+        equiv = s["equiv_flops"] / s["seconds"] / 1e12 if s["seconds"] > 0 else 0.0
         roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),
+                    "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                    "traffic_source": traffic_src,
+                    "frac_basis": "executed MFMA FLOPs (Winograd: its 16 multiplies per 2x2 tile and channel pair)",
+                    "dense_equiv_frac": round(equiv / FP32_MFMA_PEAK_TFLOPS, 4),
+                    "dense_equiv_basis": "SURVEY 8(d) dense conv MACs x 2 per second / fp32 MFMA peak (above 1 is "
+                                         "possible: Winograd executes 4/9 of the dense multiplies)",
+                    "dominant_kernel": ({"part": dom, "frac": parts[dom]["frac"],
+                                         "ms_per_step": parts[dom]["ms_per_step"]} if dom else None),
                     "kernel": "synthesis conv family (wino_kernel + the direct implicit-GEMM kernels)",
                     "launches": s["launches"],
                     "avg_launch_us": round(1e6 * s["seconds"] / max(s["launches"], 1), 2),
                     "alg_gflop_per_launch": round(s["flops"] / max(s["launches"], 1) / 1e9, 3),
                     "alg_bytes_per_launch": int(s["bytes"] / max(s["launches"], 1)),
-                    "direct_equiv_tflops": round(s["equiv_flops"] / s["seconds"] / 1e12, 3) if s["seconds"] > 0 else 0.0,
-                    "parts": {k: part(s["kinds"][k], kinds.get(k, k)) for k in sorted(s["kinds"])},
+                    "direct_equiv_tflops": round(equiv, 3),
+                    "parts": parts,
                     "share_of_step_time": round(s["seconds"] / dt_r, 4),
                     "measured": f"HIP events around every launch, {args.roofline_steps} serialised steps after the "
                                 f"timed region"}

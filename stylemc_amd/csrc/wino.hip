@@ -59,20 +59,28 @@ struct WinoParams {
     int ntn;     // output-channel blocks (cout / 32)
 };
 
-template <int TC>
+// RD selects how a lane reads its 4x4 patch from LDS.  0: 16 ds_read_b32 from the lane-linear DMA image (the 4
+// channels a half-wave reads sit SLAB apart, SLAB = 0 mod 32 floats: a 2-way bank conflict on every read).
+// 1: rows padded to CHP chunks so that SLAB = 32 mod 64 floats, and the image shifted by one float so the patch's
+// first column is 8-B aligned: 8 ds_read_b64 per patch, the 32 lanes of a group on 64 distinct banks.
+template <int TC, int RD = 0, int WT = WBT>
 struct WinoCfg {
-    static constexpr int TR = WBT / TC;             // tile rows of the block
+    static constexpr int TR = WT / TC;              // tile rows of the block
     static constexpr int ROWS = 2 * TR + 2;         // staged input rows
     static constexpr int CH = TC / 2 + 2;           // 16-B chunks per staged row (2 TC + 8 floats)
-    static constexpr int PITCH = 4 * CH;
+    static constexpr int chp(int c) { return (ROWS * 4 * c) % 64 == 32 ? c : chp(c + 1); }
+    static constexpr int CHP = RD == 0 ? CH : chp(CH);  // chunks per row in LDS (>= CH)
+    static constexpr int SHIFT = RD == 0 ? 0 : 1;   // floats the patch image is shifted by
+    static constexpr int PITCH = 4 * CHP;
     static constexpr int SLAB = ROWS * PITCH;       // floats per channel
-    static constexpr int PL = WBK * ROWS * CH;      // DMA lanes of the patch
+    static constexpr int PL = WBK * ROWS * CHP;     // DMA lanes of the patch
     static constexpr int PJ = (PL + 63) / 64;       // patch DMA wave-instructions per step
-    static constexpr int PF = PJ * 256;             // floats reserved for the patch (whole instructions)
+    static constexpr int PF = PJ * 256 + 4 * SHIFT; // floats reserved for the patch (whole instructions)
     static constexpr int UF = WBK * 16 * WBO;       // floats of the U slab
     static constexpr int UJ = UF / 256;             // U DMA wave-instructions per step (16 B per lane)
     static constexpr int STAGE = UF + PF;
     static_assert(UJ % 4 == 0, "U slab splits evenly over the 4 waves");
+    static_assert(RD == 0 || SLAB % 64 == 32, "padded slab");
 };
 
 template <int N>
@@ -85,12 +93,16 @@ __device__ __forceinline__ void wino_wait_vmcnt() {
 // 32 the LDS fragment reads.
 // OBW: 16-channel output blocks per wave (2: 4 waves of 32 channels x 16 tiles, 2 waves / SIMD; 1: 8 waves of
 // 16 channels x 16 tiles, 4 waves / SIMD -- both o-waves of a tile row transform the same patch).
-template <int TC, int OBW, int PROBE = 0>
-__global__ __launch_bounds__(64 * 8 / OBW) __attribute__((amdgpu_waves_per_eu(8 / (2 * OBW) * 1, 8 / (2 * OBW) * 1)))
+// WPE: waves per SIMD the register allocation targets (0: the OBW default, 2 for OBW 2).
+// WT: tiles per workgroup (64: 4 waves of 16 tiles; 128: 8 waves -- one U slab per step for twice the tiles, and
+// 2 TR + 2 staged rows for 2 TR output-tile rows, at one workgroup per CU).
+template <int TC, int OBW, int PROBE = 0, int RD = 0, int WPE = 0, int WT = WBT>
+__global__ __launch_bounds__(64 * 8 / OBW * WT / WBT)
+__attribute__((amdgpu_waves_per_eu(WPE ? WPE : 8 / (2 * OBW), WPE ? WPE : 8 / (2 * OBW))))
 void wino_kernel(WinoParams p) {
-    using C = WinoCfg<TC>;
-    constexpr int NW = 8 / OBW;      // waves per workgroup
-    constexpr int OW = 2 / OBW;      // o-waves per tile row of waves
+    using C = WinoCfg<TC, RD, WT>;
+    constexpr int NW = 8 / OBW * WT / WBT;  // waves per workgroup
+    constexpr int OW = 2 / OBW;             // o-waves per tile row of waves
     constexpr int TR = C::TR, ROWS = C::ROWS, CH = C::CH, PITCH = C::PITCH, SLAB = C::SLAB, STAGE = C::STAGE;
     __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
@@ -132,15 +144,15 @@ void wino_kernel(WinoParams p) {
         }
         if constexpr ((PROBE & 2) != 0)
             if (ks > 0) return;
-        float* ps = us + C::UF;
+        float* ps = us + C::UF + C::SHIFT;
 #pragma unroll
         for (int j = wave; j < C::PJ; j += NW) {
             const int L = j * 64 + lane;
-            const int c = L / (ROWS * CH);
-            const int r2 = L - c * (ROWS * CH);
-            const int r = r2 / CH, ch = r2 - r * CH;
+            const int c = L / (ROWS * C::CHP);
+            const int r2 = L - c * (ROWS * C::CHP);
+            const int r = r2 / C::CHP, ch = r2 - r * C::CHP;
             const int gyy = 2 * ty0 - 1 + r, gxx = 2 * tx0 - 4 + 4 * ch;
-            const bool ok = c < WBK && gyy >= 0 && gyy < H && gxx >= 0 && gxx < W;
+            const bool ok = c < WBK && ch < CH && gyy >= 0 && gyy < H && gxx >= 0 && gxx < W;
             const int v = (int)((((int64_t)(nn * p.cin + ci0 + c) * H + gyy) * W + gxx) * 4);
             const int msk = -(int)ok;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (__attribute__((address_space(3))) void*)(ps + j * 256),
@@ -159,7 +171,7 @@ void wino_kernel(WinoParams p) {
     const int ob16 = wo * OBW;       // first 16-channel block of this wave
     const int tl = 16 * wt + (lane & 15);
     const int tr = tl / TC, tc = tl - tr * TC;
-    const int poff = kq_lane * SLAB + 2 * tr * PITCH + 2 * tc + 3;
+    const int poff = kq_lane * SLAB + 2 * tr * PITCH + 2 * tc + 3 + C::SHIFT;
     const int uoff = (kq_lane * 4 * WBO + 16 * ob16 + (lane & 15)) * 4;
     const int yy0 = 2 * (ty0 + tr), xx0 = 2 * (tx0 + tc);
     // The MODACT epilogue's per-channel / per-pixel operands, loaded before the K loop: issued after the epilogue's
@@ -197,10 +209,21 @@ void wino_kernel(WinoParams p) {
     auto load_patch = [&](const float* ps, int kq) {
         if constexpr ((PROBE & 32) != 0) return;
         const float* pp = ps + kq * 4 * SLAB + poff;
+        if constexpr (RD == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) pd[4 * i + j] = pp[i * PITCH + j];
+                for (int j = 0; j < 4; ++j) pd[4 * i + j] = pp[i * PITCH + j];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; j += 2) {
+                    const float2 v = *reinterpret_cast<const float2*>(pp + i * PITCH + j);
+                    pd[4 * i + j] = v.x;
+                    pd[4 * i + j + 1] = v.y;
+                }
+        }
     };
     auto load_a = [&](const float* us, int gi, f32x4 (&a)[OBW]) {
         if constexpr ((PROBE & 32) != 0) {
@@ -259,7 +282,7 @@ void wino_kernel(WinoParams p) {
             if (has_s) { sn[0] = srow[(ks + 1) * WBK]; sn[1] = srow[(ks + 1) * WBK + 4]; }
         }
         const float* us = smem + (ks & 1) * STAGE;
-        const float* ps = us + C::UF;
+        const float* ps = us + C::UF;   // (the patch image starts C::SHIFT floats further; poff includes it)
         // (sched_barrier fences keep each phase where it is written: the compiler would otherwise sink the
         // prefetches next to their use to save registers and wait on them with lgkmcnt(0))
         load_patch(ps, 0);
@@ -413,10 +436,10 @@ __global__ __launch_bounds__(256) void wino_weights_kernel(const float* w, int c
 }
 
 // tile columns of a workgroup's block: 64, 32 or 16 (the kernel's instantiations), dividing the tile grid
-int wino_tc(int h, int w) {
+int wino_tc(int h, int w, int wt = WBT) {
     if (h % 2 || w % 4 || w < 32) return 0;
     for (int tc = 64; tc >= 16; tc /= 2)
-        if ((w / 2) % tc == 0 && (h / 2) % (WBT / tc) == 0) return tc;
+        if ((w / 2) % tc == 0 && (h / 2) % (wt / tc) == 0) return tc;
     return 0;
 }
 
