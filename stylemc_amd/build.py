@@ -22,6 +22,10 @@ ARCH = os.environ.get("SMC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-I", INCLUDE,
           "-munsafe-fp-atomics", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+# per-source extra flags: the Winograd kernel's transform runs beside its MFMAs, where packed f32 VALU (what the SLP
+# vectorizer makes of adjacent scalar adds, plus the register moves that pair them) costs more than scalar ops
+# (MI355X_MICROARCH.md 'price of one filler beside MFMAs'; tools/probes/wino_ab.hip: 3-5 % per launch)
+FILE_FLAGS = {"wino.hip": ["-fno-slp-vectorize"]}
 
 
 def sources():
@@ -39,7 +43,7 @@ def _compile(src):
     obj = os.path.join(OUT_DIR, os.path.basename(src)[:-4] + ".o")
     headers = glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(INCLUDE, "*.h"))
     if _stale(obj, [src] + headers):
-        cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
+        cmd = [HIPCC] + CFLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed on {src}:\n{r.stdout}\n{r.stderr}")

@@ -1,6 +1,6 @@
 // A/B harness for Winograd kernel variants on random data (the DVFS clock depends on the operands: zero-filled
 // inputs run faster, MI355X_MICROARCH.md 'DVFS give-back').  Compiles csrc/wino.hip into this translation unit and
-// times two wino_kernel variants <TC, 2, 0, RD, 0, WT> (RD: patch read form, WT: tiles per workgroup) on the
+// times two wino_kernel variants <TC, SM, PERSIST, PROBE> on the
 // synthesis conv1 shapes (FFHQ-1024, batch 4), interleaved, and checks that the outputs are bit-identical.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include tools/probes/wino_ab.hip stylemc_amd/csrc/errors.hip \
 //         -o tools/probes/wino_ab && tools/probes/wino_ab
@@ -27,23 +27,38 @@ __global__ void fill_kernel(float* p, size_t n, unsigned seed, float scale, floa
     }
 }
 
-template <int TC, int RD, int WT>
-void launch(const WinoParams& p, int r, int n, int c) {
+template <int SM_, int PERSIST_, int PROBE_ = 0>
+struct V {
+    static constexpr int SM = SM_, PERSIST = PERSIST_, PROBE = PROBE_;
+};
+
+template <int TC, int SM, int PERSIST, int PROBE>
+void launch_i(const WinoParams& p, int r, int n, int c) {
     WinoParams q = p;
     q.gx = (r / 2) / TC;
-    q.gy = (r / 2) / (WT / TC);
+    q.gy = (r / 2) / (WBT / TC);
     q.ntn = c / WBO;
-    const int wgs = n * q.gx * q.gy * q.ntn;
-    hipLaunchKernelGGL((wino_kernel<TC, 2, 0, RD, 0, WT>), dim3(wgs), dim3(256 * WT / 64), 0, 0, q);
+    const int items = n * q.gx * q.gy * q.ntn;
+    if (PERSIST) {
+        launch_wino<TC, SM, 0>(q, items, 0);
+    } else {
+        auto kern = &wino_kernel<TC, SM, 0, 0, PROBE>;
+        hipLaunchKernelGGL(kern, dim3(items), dim3(256), 0, 0, q);
+    }
 }
 
-template <int TC, int RD, int WT>
+template <int TC, class VV>
+void launch(const WinoParams& p, int r, int n, int c) {
+    launch_i<TC, VV::SM, VV::PERSIST, VV::PROBE>(p, r, n, c);
+}
+
+template <int TC, class VV>
 float time_kernel(const WinoParams& p, int r, int n, int c, int reps) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
     (void)hipEventRecord(a, 0);
-    for (int i = 0; i < reps; ++i) launch<TC, RD, WT>(p, r, n, c);
+    for (int i = 0; i < reps; ++i) launch<TC, VV>(p, r, n, c);
     (void)hipEventRecord(b, 0);
     (void)hipEventSynchronize(b);
     float ms = 0.f;
@@ -53,9 +68,14 @@ float time_kernel(const WinoParams& p, int r, int n, int c, int reps) {
     return 1e3f * ms / reps;
 }
 
-// variant A = <TC, RDA, WTA>, variant B = <TC, RDB, WTB>
-template <int TC, int RDA, int WTA, int RDB, int WTB>
-int run(int r, double* tot) {
+template <class VV>
+void name(char* buf) {
+    std::snprintf(buf, 64, "SM%d,PERSIST%d,PROBE%d", VV::SM, VV::PERSIST, VV::PROBE);
+}
+
+// variant A vs variant B at shape r (with_s: the style-scaled forward; else the data gradient's plain conv)
+template <int TC, class VA, class VB>
+int run(int r, bool with_s, double* tot) {
     const int n = 4, c = std::min(32768 / r, 512);
     const size_t xe = (size_t)n * c * r * r, ue = (size_t)16 * c * c;
     float *x, *y0, *y1, *uw, *s;
@@ -68,14 +88,14 @@ int run(int r, double* tot) {
     hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, uw, ue, 2u, 0.2f, 0.f);
     hipLaunchKernelGGL(fill_kernel, dim3(16), dim3(256), 0, 0, s, (size_t)n * c, 3u, 1.f, 1.f);
     WinoParams p{};
-    p.x = x; p.n = n; p.cin = c; p.h = r; p.w = r; p.cout = c; p.uw = uw; p.s = s;
+    p.x = x; p.n = n; p.cin = c; p.h = r; p.w = r; p.cout = c; p.uw = uw; p.s = with_s ? s : nullptr;
     p.mode = SMC_EPI_STORE; p.act = SMC_ACT_LINEAR; p.gain = 1.f; p.clamp = -1.f;
     p.ext.rs = 1;
     const double flops = 2.0 * n * c * c * (r / 2) * (r / 2) * 16;
     p.y = y0;
-    launch<TC, RDA, WTA>(p, r, n, c);
+    launch<TC, VA>(p, r, n, c);
     p.y = y1;
-    launch<TC, RDB, WTB>(p, r, n, c);
+    launch<TC, VB>(p, r, n, c);
     CK(hipDeviceSynchronize());
     std::vector<float> h0(xe), h1(xe);
     CK(hipMemcpy(h0.data(), y0, xe * 4, hipMemcpyDeviceToHost));
@@ -85,16 +105,19 @@ int run(int r, double* tot) {
     const int reps = 10, rounds = 3;
     for (int k = 0; k < rounds; ++k) {  // interleaved
         p.y = y0;
-        t[0] += time_kernel<TC, RDA, WTA>(p, r, n, c, reps);
+        t[0] += time_kernel<TC, VA>(p, r, n, c, reps);
         p.y = y1;
-        t[1] += time_kernel<TC, RDB, WTB>(p, r, n, c, reps);
+        t[1] += time_kernel<TC, VB>(p, r, n, c, reps);
     }
     for (int v = 0; v < 2; ++v) {
         t[v] /= rounds;
         tot[v] += t[v];
     }
-    std::printf("r=%5d c=%4d TC=%2d  A(RD%d,WT%d) %7.1f us (frac %.3f)  B(RD%d,WT%d) %7.1f us (frac %.3f)  %+.1f%%  "
-                "outputs %s\n", r, c, TC, RDA, WTA, t[0], flops / (t[0] * 1e-6) / 157.3e12, RDB, WTB, t[1],
+    char na[64], nb[64];
+    name<VA>(na);
+    name<VB>(nb);
+    std::printf("r=%5d c=%4d TC=%2d %s  A(%s) %7.1f us (frac %.3f)  B(%s) %7.1f us (frac %.3f)  %+.1f%%  outputs %s\n",
+                r, c, TC, with_s ? "fwd" : "bwd", na, t[0], flops / (t[0] * 1e-6) / 157.3e12, nb, t[1],
                 flops / (t[1] * 1e-6) / 157.3e12, 100.0 * (t[0] / t[1] - 1.0), same ? "bit-identical" : "DIFFER");
     CK(hipFree(x)); CK(hipFree(y0)); CK(hipFree(y1)); CK(hipFree(uw)); CK(hipFree(s));
     return same ? 0 : 2;
@@ -103,12 +126,14 @@ int run(int r, double* tot) {
 int main() {
     double tot[2] = {0, 0};
     int rc = 0;
-    rc |= run<32, 0, 64, 0, 128>(64, tot);
-    rc |= run<64, 0, 64, 0, 128>(128, tot);
-    rc |= run<64, 0, 64, 0, 128>(256, tot);
-    rc |= run<64, 0, 64, 0, 128>(512, tot);
-    rc |= run<64, 0, 64, 0, 128>(1024, tot);
-    rc |= run<64, 0, 64, 1, 128>(1024, tot);
+    rc |= run<16, V<1, 0>, V<1, 1>>(32, true, tot);
+    rc |= run<32, V<1, 0>, V<1, 1>>(64, true, tot);
+    rc |= run<64, V<1, 0>, V<1, 1>>(128, true, tot);
+    rc |= run<64, V<1, 0>, V<1, 1>>(256, true, tot);
+    rc |= run<64, V<1, 0>, V<1, 1>>(512, true, tot);
+    rc |= run<64, V<1, 0>, V<1, 1>>(1024, true, tot);
+    rc |= run<64, V<2, 0>, V<2, 1>>(512, false, tot);
+    rc |= run<64, V<2, 0>, V<2, 1>>(1024, false, tot);
     std::printf("total A %.1f us  B %.1f us  (%+.1f%%)\n", tot[0], tot[1], 100.0 * (tot[0] / tot[1] - 1.0));
     return rc;
 }
