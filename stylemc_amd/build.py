@@ -16,8 +16,11 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(REPO, "include")
-OUT_DIR = os.path.join(PKG, "_lib")
+# A/B builds only (tools/): SMC_AB_OUT puts a variant library in its own directory, SMC_AB_DEFINES adds -D flags.
+# The product build (no variables set) is the one stylemc_amd._hip loads.
+OUT_DIR = os.environ.get("SMC_AB_OUT") or os.path.join(PKG, "_lib")
 LIB = os.path.join(OUT_DIR, "libstylemc_hip.so")
+AB_DEFINES = [f"-D{d}" for d in os.environ.get("SMC_AB_DEFINES", "").split()]
 ARCH = os.environ.get("SMC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-I", INCLUDE,
@@ -43,7 +46,7 @@ def _compile(src):
     obj = os.path.join(OUT_DIR, os.path.basename(src)[:-4] + ".o")
     headers = glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(INCLUDE, "*.h"))
     if _stale(obj, [src] + headers):
-        cmd = [HIPCC] + CFLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
+        cmd = [HIPCC] + CFLAGS + AB_DEFINES + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed on {src}:\n{r.stdout}\n{r.stderr}")

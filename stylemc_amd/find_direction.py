@@ -132,7 +132,8 @@ class DirectionFinder:
     def __init__(self, G, styles_array, clip_losses, id_loss, resolution=1024, batch_size=4, learning_rate=1.5,
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
-                 overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None, G2=None, temp_shapes2=None):
+                 overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None, G2=None, temp_shapes2=None,
+                 prefetch_id=True):
         self.G = G
         # the edited image's generator (train_latent_mapper.py:100-106,159-162 --network2; default G itself)
         self.G_edit = G2 if G2 is not None else G
@@ -144,6 +145,10 @@ class DirectionFinder:
         # on the S codes of the next batch, not on the direction) runs on a third stream during this
         # iteration's backward; every iteration still synthesises its own original image exactly once
         self.prefetch_orig = prefetch_orig
+        # ... and that image's IR-SE50 features (no gradient): IR-SE50 is the loss network that bounds the step
+        # (tools/sensitivity.py: dropping it saves 1.8 ms, dropping CLIP nothing), so its critical-path share is
+        # cut to the edited images' forward + backward; CLIP keeps the [edited; original] batch
+        self.prefetch_id = prefetch_id
         self._next_i = None
         self._pref = None
         # edited + original image through each loss network as ONE batch (backward for the edited half)
@@ -231,12 +236,16 @@ class DirectionFinder:
         rows); then each loss network sees [edited; original] as one batch."""
         side = self._side_stream()
         pref, self._pref = self._pref, None
+        y_feats = None
         if side is not None and pref is not None and pref[0] == key:
             main = torch.cuda.current_stream()
             img = self._synth_edited(styles, d)
             main.wait_stream(self._pre)
             orig = pref[1]
             orig.record_stream(main)
+            y_feats = pref[2]
+            if y_feats is not None:
+                y_feats.record_stream(main)
         elif side is not None:
             main = torch.cuda.current_stream()
             side.wait_stream(main)
@@ -259,7 +268,8 @@ class DirectionFinder:
             # them where the gradients meet (d img)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                id_terms = self.id_loss.per_sample_pair(img, orig)
+                id_terms = (self.id_loss.per_sample_with(img, y_feats) if y_feats is not None
+                            else self.id_loss.per_sample_pair(img, orig))
         else:
             id_terms = self.id_loss.per_sample_pair(img, orig)
         clip_terms = sum(w * cl.per_sample_pair(t, s) for (cl, w), (t, s) in zip(self.clip_losses,
@@ -332,7 +342,8 @@ class DirectionFinder:
         self._pre.wait_event(self._fwd_done)
         with torch.cuda.stream(self._pre), torch.no_grad():
             orig = self.synth_fn(self.G, self.until_k, self.styles_array[a:b], self.temp_shapes, self.noise_mode)
-        self._pref = ((a, b), orig)
+            feats = self.id_loss.target_feats(orig) if self.prefetch_id else None
+        self._pref = ((a, b), orig, feats)
 
     def step(self):
         self.it += 1

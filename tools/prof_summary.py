@@ -22,10 +22,21 @@ def is_family(name):  # TAG 0 and TAG 1 (reported separately below)
     return any(f in name for f in FAMILY)
 
 
+def load_rows(path):
+    """Kernel dispatches as dicts with the CSV trace's keys: from a --output-format csv kernel trace, or from the
+    rocpd SQLite database rocprofv3 writes by default (ROCm 7.2: `<name>_results.db`, view `kernels`)."""
+    if path.endswith(".db"):
+        import sqlite3
+        con = sqlite3.connect(path)
+        return [{"Kernel_Name": n, "Start_Timestamp": a, "End_Timestamp": b}
+                for n, a, b in con.execute("select name, start, end from kernels")]
+    return list(csv.DictReader(open(path)))
+
+
 def main():
     path = sys.argv[1]
     steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else None
-    rows = list(csv.DictReader(open(path)))
+    rows = load_rows(path)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     first = next(i for i, r in enumerate(rows) if is_family(r["Kernel_Name"]))
     rows = rows[first:]
