@@ -59,6 +59,9 @@ _SIGS = {
     "smc_conv3x3_wino_supported": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "smc_conv3x3_wino_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P]),
     "smc_wino_weights_f32": (c_int, [P, c_int, c_int, c_int, P, P]),
+    "smc_conv3x3_wino4_supported": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "smc_conv3x3_wino4_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P]),
+    "smc_wino4_weights_f32": (c_int, [P, c_int, c_int, c_int, P, P]),
     "smc_modconv_epilogue_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, P, P]),
     "smc_modconv_blur_act_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                          c_int, c_int, c_int, c_int, c_float, c_int, P, P]),

@@ -28,7 +28,7 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch=
 # per-source extra flags: the Winograd kernel's transform runs beside its MFMAs, where packed f32 VALU (what the SLP
 # vectorizer makes of adjacent scalar adds, plus the register moves that pair them) costs more than scalar ops
 # (MI355X_MICROARCH.md 'price of one filler beside MFMAs'; tools/probes/wino_ab.hip: 3-5 % per launch)
-FILE_FLAGS = {"wino.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"wino.hip": ["-fno-slp-vectorize"], "wino4.hip": ["-fno-slp-vectorize"]}
 
 
 def sources():

@@ -1,0 +1,526 @@
+// Winograd F(4x4, 3x3) convolution on fp32 MFMA for gfx950 (v_mfma_f32_16x16x4_f32).
+//
+// The same 3x3 stride-1 'same' convolutions as wino.hip (SynthesisLayer conv1 forward and data gradient,
+// conv2d_resample.py:147-154), with 4x4 output tiles: each tile comes from a 6x6 input patch with 36 multiplies per
+// (input, output) channel pair instead of 144 (4x fewer MFMA FLOPs; F(2x2) saves 2.25x):
+//     V = B^T d B   (6x6)        U = G g G^T   (6x6, frozen: smc_wino4_weights_f32, computed in fp64)
+//     M[xi] = sum_c U[xi][c][o] * V[xi][c][t]      (36 independent GEMMs on the matrix core)
+//     Y = A^T M A   (4x4)
+// with the interpolation points 0, 1, -1, 2, -2 (Lavin & Gray):
+//   B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
+//   G   = [1/4 0 0; -1/6 -1/6 -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1]
+//   A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
+// Index xi = 6 b + a for the element (row a, column b) of the 6x6 transform domain.
+//
+// Work decomposition (512 threads = 8 waves, one workgroup per CU, 2 waves per SIMD):
+//   * a work item is 16 CG output channels x 16 TG tiles (TG tile rows x 16 tile columns = 4 TG x 64 outputs of
+//     one image); wave w owns channel group w % CG and tile row w / CG: 16 channels x 16 tiles, all 36 xi = 36
+//     accumulators of the 16x16x4 MFMA (144 registers).  A lane holds one tile and 4 channels of each, so the 36
+//     M values of a (channel, tile) sit in one lane and the output transform + modconv epilogue are lane-local.
+//   * K steps of 4 input channels (the MFMA's k).  V is computed ONCE per workgroup and shared through LDS by the
+//     CG channel groups: per step, TG waves (alternating halves of the workgroup, so every SIMD carries the same
+//     transform load over two steps) each transform 64 patches (one per lane: 36 reads, 2 x 6 six-point
+//     transforms, x s[n, c], 9 ds_write_b128), the other waves only issue MFMAs.  The transform of step k + 1 runs
+//     under the MFMAs of step k.
+//   * Operands by DMA (buffer_load ... lds): the U slab [4][9][16 CG][4] one step ahead, the raw input rows of the
+//     block's (4 TG + 2) x 72 patch two steps ahead (16-B chunks from column 4 tx0 - 4; the buffer range check
+//     zero-fills the image border).  LDS: 2 x (U + patch + V) = 132 KiB (CG 4) / 150 KiB (CG 2); one barrier per
+//     step.
+#include <algorithm>
+#include <type_traits>
+
+#include "common.hpp"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int W4K = 4;       // input channels per K step (= the MFMA's k)
+constexpr int NXQ = 9;       // xi quads (36 / 4)
+constexpr int PCH = 18;      // 16-B chunks per staged patch row
+constexpr int PPITCH = 72;   // floats per staged patch row (columns 4 tx0 - 4 .. 4 tx0 + 67)
+constexpr int SENTINEL = 0x7ffffff0;
+
+struct Wino4Params {
+    const float* x;
+    int n, cin, h, w;
+    float* y;
+    int cout;
+    const float* uw;  // [cin][9][cout][4]
+    const float* s;   // [n][cin] or NULL
+    int mode;
+    const float* d;
+    const float* noise;
+    int64_t noise_nstride;
+    const float* noise_strength;
+    const float* bias;
+    int act;
+    float alpha, gain, clamp;
+    float* u_save;
+    smc::EpiExt ext;
+    int gx, gy;  // tile blocks per image along x / y
+    int ntn;     // output-channel blocks (cout / (16 CG))
+};
+
+template <int CG, int TG>
+struct W4Cfg {
+    static_assert(CG * TG == 8, "8 waves");
+    static constexpr int OB = 16 * CG;                 // output channels per work item
+    static constexpr int TB = 16 * TG;                 // tiles per work item
+    static constexpr int ROWS = 4 * TG + 2;            // staged input rows
+    static constexpr int SLAB = ROWS * PPITCH;         // patch floats per channel
+    static constexpr int UJ = W4K * NXQ * OB / 64;     // U DMA wave-instructions per step (16 B per lane)
+    static constexpr int PL = W4K * ROWS * PCH;        // patch DMA lanes per step
+    static constexpr int PJ = (PL + 63) / 64;
+    static constexpr int UF = UJ * 256;                // floats
+    static constexpr int PF = PJ * 256;                // floats (whole instructions)
+    static constexpr int VF = W4K * NXQ * TB * 4;      // floats
+    static constexpr int STAGE = UF + PF + VF;
+    static constexpr int UJW = (UJ + 7) / 8;
+    static constexpr int PJW = (PJ + 7) / 8;
+    static_assert(W4K * TB == 64 * TG, "one patch per lane of TG waves");
+};
+
+template <int N>
+__device__ __forceinline__ void w4_wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// six-point input transform y = B^T x (14 VALU)
+__device__ __forceinline__ void bt6(const float (&x)[6], float (&y)[6]) {
+    y[0] = __fmaf_rn(4.f, x[0], __fmaf_rn(-5.f, x[2], x[4]));
+    const float p = x[1] + x[2], q = x[3] + x[4];
+    y[1] = __fmaf_rn(-4.f, p, q);
+    const float r = x[1] - x[2], s = x[4] - x[3];
+    y[2] = __fmaf_rn(4.f, r, s);
+    const float u = x[3] - x[1], w = x[4] - x[2];
+    y[3] = __fmaf_rn(2.f, u, w);
+    y[4] = __fmaf_rn(-2.f, u, w);
+    y[5] = __fmaf_rn(4.f, x[1], __fmaf_rn(-5.f, x[3], x[5]));
+}
+
+// six-point output transform z = A^T m (4 outputs)
+__device__ __forceinline__ void at6(const float (&m)[6], float (&z)[4]) {
+    const float s12 = m[1] + m[2], d12 = m[1] - m[2], s34 = m[3] + m[4], d34 = m[3] - m[4];
+    z[0] = m[0] + s12 + s34;
+    z[1] = __fmaf_rn(2.f, d34, d12);
+    z[2] = __fmaf_rn(4.f, s34, s12);
+    z[3] = __fmaf_rn(8.f, d34, d12) + m[5];
+}
+
+struct W4Item {
+    int nn, ty0, tx0, o0;
+};
+
+// SM: style scale s[n, c] (1: present, 2: absent).  EK: epilogue body (1: MODACT lrelu + gain + clamp, 2: MODACT
+// linear, 0: any mode through smc::epi_y / epi_ext_apply).  PROBE (0 in the library; tools/probes/wino4_probe.hip)
+// removes pieces for timing: 1 the U DMAs after step 0, 2 the patch DMAs after step 1, 4 the transform, 8 the
+// per-step wait + barrier.
+template <int CG, int TG, int SM, int EK, int PROBE = 0>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void wino4_kernel(Wino4Params p) {
+    using C = W4Cfg<CG, TG>;
+    constexpr int OB = C::OB, TB = C::TB, ROWS = C::ROWS, SLAB = C::SLAB, STAGE = C::STAGE;
+    constexpr int UJ = C::UJ, PJ = C::PJ, UJW = C::UJW, PJW = C::PJW;
+    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cg = wave % CG, tg = wave / CG;
+    const int H = p.h, W = p.w;
+    const int64_t plane = (int64_t)H * W;
+    const int nsteps = p.cin / W4K;
+    const int total = p.n * p.gx * p.gy * p.ntn;
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * plane * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ursrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.uw, (short)0, p.cin * 36 * p.cout * 4, 0x00020000);
+
+    const int v = blockIdx.x;
+    if (v >= total) return;
+    // work item -> (image, tile block, output-channel block) in the XCD-aware bijective order of wino.hip
+    // (output-channel blocks fastest: the workgroups that stage the same input patch share an L2)
+    W4Item it;
+    {
+        const int xcd = v % 8, q8 = total / 8, r8 = total % 8;
+        const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + v / 8;
+        const int ob = id % p.ntn, tgi = id / p.ntn;
+        const int per_img = p.gx * p.gy;
+        it.nn = tgi / per_img;
+        const int rem = tgi - it.nn * per_img;
+        it.ty0 = (rem / p.gx) * TG;
+        it.tx0 = (rem % p.gx) * 16;
+        it.o0 = ob * OB;
+    }
+
+    // per-lane DMA byte offsets of step 0 (a step adds a scalar offset)
+    // U: 16-B lane L = (wave + 8 j) 64 + lane = run * OB + o (run = c * 9 + xq); instruction j adds 512 / OB runs,
+    // a scalar offset
+    int pv[PJW];
+    const int uv0 = (((wave * 64 + lane) / OB) * p.cout + it.o0 + (wave * 64 + lane) % OB) * 16;
+    const int ujs = (512 / OB) * p.cout * 16;
+#pragma unroll
+    for (int jj = 0; jj < PJW; ++jj) {
+        const int L = (wave + 8 * jj) * 64 + lane;  // = (c * ROWS + r) * PCH + ch
+        const int c = L / (ROWS * PCH);
+        const int r2 = L - c * (ROWS * PCH);
+        const int r = r2 / PCH, ch = r2 - r * PCH;
+        const int gyy = 4 * it.ty0 - 1 + r, gxx = 4 * it.tx0 - 4 + 4 * ch;
+        const bool ok = c < W4K && gyy >= 0 && gyy < H && gxx >= 0 && gxx < W;
+        pv[jj] = ok ? (int)((((int64_t)(it.nn * p.cin + c) * H + gyy) * W + gxx) * 4) : SENTINEL;
+    }
+    const int ustep = NXQ * W4K * p.cout * 16;       // bytes of U per K step
+    const int pstep = W4K * (int)plane * 4;           // bytes of input per K step
+    auto issue_u = [&](int ks, int slot) {
+        if constexpr ((PROBE & 1) != 0)
+            if (ks > 0) return;
+        float* us = smem + slot * STAGE;
+#pragma unroll
+        for (int j = 0; j < UJW; ++j)
+            if (wave + 8 * j < UJ)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    ursrc, (__attribute__((address_space(3))) void*)(us + (wave + 8 * j) * 256), 16, uv0,
+                    ks * ustep + j * ujs, 0, 0);
+    };
+    auto issue_p = [&](int ks, int slot) {
+        if constexpr ((PROBE & 2) != 0)
+            if (ks > 1) return;
+        float* ps = smem + slot * STAGE + C::UF;
+#pragma unroll
+        for (int jj = 0; jj < PJW; ++jj)
+            if (wave + 8 * jj < PJ) {
+                const int vo = pv[jj];
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    xrsrc, (__attribute__((address_space(3))) void*)(ps + (wave + 8 * jj) * 256), 16, vo, ks * pstep, 0, 0);
+            }
+    };
+
+    // transform role: V of step j is computed by waves [(j & 1) TG, (j & 1) TG + TG), lane -> one (channel, tile)
+    const int kq_lane = lane >> 4;
+    const int fa_off = (kq_lane * NXQ * OB + 16 * cg + (lane & 15)) * 4;   // A fragment (xq 0) in a U slot
+    const int fb_off = (kq_lane * NXQ * TB + 16 * tg + (lane & 15)) * 4;   // B fragment (xq 0) in a V slot
+    const int tw_rel = wave % TG;  // this wave's index among the transform waves of its half
+    const int tpi = tw_rel * 64 + lane;
+    const int tc_ch = tpi / TB, tc_t = tpi - tc_ch * TB;
+    const int p_off = tc_ch * SLAB + 4 * (tc_t / 16) * PPITCH + 4 * (tc_t % 16) + 3;
+    const int v_off = (tc_ch * NXQ * TB + tc_t) * 4;
+    const float* srow = SM == 1 ? p.s + (int64_t)it.nn * p.cin + tc_ch : nullptr;
+    // transform waves of step j: waves 0-3 / 4-7 (TG 4), 0-1 / 2-3 (TG 2) for even / odd j
+    auto tw_step = [&](int j) -> bool {
+        if constexpr (TG == 4) return (wave >> 2) == (j & 1);
+        else return (wave >> 1) == (j & 1);
+    };
+
+    // The transform runs per column pair bp (xi = 6 b + a, b = 2 bp, 2 bp + 1: 12 consecutive values = 3 quads):
+    // the row pass of the pair's two columns over the 6 patch rows (read from LDS again per pair: 12 live values
+    // instead of 36), then the column pass of the two columns, x s[n, c], and 3 ds_write_b128 into the V slot.
+    auto rows_part = [&](int slot, int bp, int i0, float (&rt2)[6][2]) {
+        float xr[3][6];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float* pp = smem + slot * STAGE + C::UF + p_off + (i0 + k) * PPITCH;
+            const f32x4 m = *reinterpret_cast<const f32x4*>(pp + 1);
+            xr[k][1] = m[0]; xr[k][2] = m[1]; xr[k][3] = m[2]; xr[k][4] = m[3];
+            xr[k][0] = bp == 0 ? pp[0] : 0.f;
+            xr[k][5] = bp == 2 ? pp[5] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float* x = xr[k];
+            float y0, y1;
+            if (bp == 0) {  // (d B)[i][0], [i][1]
+                y0 = __fmaf_rn(4.f, x[0], __fmaf_rn(-5.f, x[2], x[4]));
+                y1 = __fmaf_rn(-4.f, x[1] + x[2], x[3] + x[4]);
+            } else if (bp == 1) {  // [i][2], [i][3]
+                y0 = __fmaf_rn(4.f, x[1] - x[2], x[4] - x[3]);
+                y1 = __fmaf_rn(2.f, x[3] - x[1], x[4] - x[2]);
+            } else {  // [i][4], [i][5]
+                y0 = __fmaf_rn(-2.f, x[3] - x[1], x[4] - x[2]);
+                y1 = __fmaf_rn(4.f, x[1], __fmaf_rn(-5.f, x[3], x[5]));
+            }
+            rt2[i0 + k][0] = y0;
+            rt2[i0 + k][1] = y1;
+        }
+    };
+    auto col_part = [&](int bp, float sc, int slot, const float (&rt2)[6][2]) {
+        float vq[12];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            float x[6], y[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) x[i] = rt2[i][bb];
+            bt6(x, y);
+#pragma unroll
+            for (int a = 0; a < 6; ++a) vq[6 * bb + a] = SM == 1 ? y[a] * sc : y[a];
+        }
+        float* vs = smem + slot * STAGE + C::UF + C::PF + v_off;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            *reinterpret_cast<f32x4*>(vs + (3 * bp + q) * TB * 4) =
+                f32x4{vq[4 * q], vq[4 * q + 1], vq[4 * q + 2], vq[4 * q + 3]};
+    };
+
+    f32x4 acc[36];
+#pragma unroll
+    for (int xi = 0; xi < 36; ++xi) acc[xi] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // ---- prologue: U(0), P(0), P(1); V(0)
+    issue_u(0, 0);
+    issue_p(0, 0);
+    if (nsteps > 1) issue_p(1, 1);
+    w4_wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    // style scales of the transform: the value for V(k + 1) is loaded during step k - 1 (a global load issued at
+    // the use would stall the transform waves for its round trip every step)
+    float s_nx = SM == 1 && nsteps > 1 ? srow[W4K] : 1.f;
+    if (tw_step(0)) {
+        const float sc = SM == 1 ? srow[0] : 1.f;
+#pragma unroll
+        for (int bp = 0; bp < 3; ++bp) {
+            float rt2[6][2];
+            rows_part(0, bp, 0, rt2);
+            rows_part(0, bp, 3, rt2);
+            col_part(bp, sc, 0, rt2);
+        }
+    }
+
+    // ---- K loop: MFMAs of step k (U slot k & 1, V slot k & 1) with V(k + 1) built by the transform waves
+    // (one body with wave-uniform branches around the transform pieces: two specialised bodies behind one branch
+    // make the compiler merge the accumulators of both at the loop head, which spills them)
+    auto step = [&](int ks, bool tw) {
+        f32x4 fa[2], fb[2];
+        float rt2[6][2];
+        const int sl = ks & 1;
+        const float* us = smem + sl * STAGE + fa_off;
+        const float* vs = smem + sl * STAGE + C::UF + C::PF + fb_off;
+        const float sc = s_nx;
+        if (SM == 1 && ks + 2 < nsteps) s_nx = srow[(ks + 2) * W4K];
+        fa[0] = *reinterpret_cast<const f32x4*>(us);
+        fb[0] = *reinterpret_cast<const f32x4*>(vs);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int xq = 0; xq < NXQ; ++xq) {
+            if (xq + 1 < NXQ) {
+                fa[(xq + 1) & 1] = *reinterpret_cast<const f32x4*>(us + (xq + 1) * OB * 4);
+                fb[(xq + 1) & 1] = *reinterpret_cast<const f32x4*>(vs + (xq + 1) * TB * 4);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[4 * xq + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[xq & 1][j], fb[xq & 1][j], acc[4 * xq + j], 0, 0, 0);
+            if ((PROBE & 4) == 0 && tw) {  // V(k + 1), one third of a column pair per MFMA group
+                if (xq % 3 == 2) col_part(xq / 3, sc, sl ^ 1, rt2);
+                else rows_part(sl ^ 1, xq / 3, 3 * (xq % 3), rt2);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    for (int ks = 0; ks < nsteps; ++ks) {
+        if constexpr ((PROBE & 8) == 0) {
+            w4_wait_vmcnt<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // U(k), P(k + 1) landed, V(k) written; step k - 1's slots are free
+        }
+        asm volatile("" ::: "memory");
+        if (ks + 1 < nsteps) issue_u(ks + 1, (ks + 1) & 1);
+        if (ks + 2 < nsteps) issue_p(ks + 2, ks & 1);
+        step(ks, ks + 1 < nsteps && tw_step(ks + 1));
+    }
+
+    // ---- epilogue: Y = A^T M A per (channel, tile), then the conv epilogue
+    const int nn = it.nn;
+    const int yy0 = 4 * (it.ty0 + tg), xx0 = 4 * (it.tx0 + (lane & 15));
+    float nz[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nz[i][j] = 0.f;
+    float e_d[4], e_b[4];
+    if (p.mode == SMC_EPI_MODACT) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int o = it.o0 + 16 * cg + 4 * kq_lane + r;
+            e_d[r] = (p.d ? p.d[(int64_t)nn * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
+            e_b[r] = p.bias ? p.bias[o] : 0.f;
+        }
+        if (p.noise) {
+            const float nstr = p.noise_strength ? *p.noise_strength : 1.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const f32x4 q = *reinterpret_cast<const f32x4*>(p.noise + nn * p.noise_nstride + (int64_t)(yy0 + i) * W + xx0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) nz[i][j] = q[j] * nstr;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int o = it.o0 + 16 * cg + 4 * kq_lane + r;
+        float zc[4][6];  // A^T M: zc[p][b]
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+            float m[6], z[4];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) m[a] = acc[6 * b + a][r];
+            at6(m, z);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) zc[q][b] = z[q];
+        }
+        const int64_t obase = ((int64_t)nn * p.cout + o) * plane;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float out[4];
+            at6(zc[i], out);
+            const int64_t idx = obase + (int64_t)(yy0 + i) * W + xx0;
+            float q[4];
+            if (EK != 0 || p.mode == SMC_EPI_MODACT) {
+                if (p.u_save) *reinterpret_cast<f32x4*>(p.u_save + idx) = f32x4{out[0], out[1], out[2], out[3]};
+                const float dsc = e_d[r], bo = e_b[r];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if constexpr (EK == 1) {
+                        const float z = __fmaf_rn(out[j], dsc, nz[i][j]) + bo;
+                        q[j] = fmaxf(fminf(fmaxf(z, z * p.alpha) * p.gain, p.clamp), -p.clamp);
+                    } else if constexpr (EK == 2) {
+                        q[j] = (__fmaf_rn(out[j], dsc, nz[i][j]) + bo) * p.gain;
+                    } else {
+                        q[j] = smc::epi_y(out[j], dsc, nz[i][j], bo, p.act, p.alpha, p.gain, p.clamp);
+                        if (p.ext.residual)
+                            q[j] = smc::epi_ext_apply(SMC_EPI_STORE, q[j], nn, o, idx + j, yy0 + i, xx0 + j, p.cout, H,
+                                                      W, nullptr, nullptr, p.ext);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    q[j] = smc::epi_ext_apply(p.mode, out[j], nn, o, idx + j, yy0 + i, xx0 + j, p.cout, H, W, p.bias,
+                                              p.u_save, p.ext);
+            }
+            *reinterpret_cast<f32x4*>(p.y + idx) = f32x4{q[0], q[1], q[2], q[3]};
+        }
+    }
+}
+
+// U = G g G^T per (k, n) in fp64, rounded once: flip = 0: g = w[n][k] (k = cin, n = cout: the forward
+// correlation); flip = 1: g = w[k][n] rotated by 180 degrees (k = cout, n = cin: the data gradient).
+// Out: [K][9][N][4], element xi = 6 b + a of the 6x6 U at [k][xi / 4][n][xi % 4].
+__global__ __launch_bounds__(256) void wino4_weights_kernel(const float* w, int cout, int cin, int flip, float* uw) {
+    const int K = flip ? cout : cin, N = flip ? cin : cout;
+    const int64_t total = (int64_t)K * N;
+    const double Gm[6][3] = {{0.25, 0., 0.},
+                             {-1. / 6., -1. / 6., -1. / 6.},
+                             {-1. / 6., 1. / 6., -1. / 6.},
+                             {1. / 24., 1. / 12., 1. / 6.},
+                             {1. / 24., -1. / 12., 1. / 6.},
+                             {0., 0., 1.}};
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(e / N), nidx = (int)(e - (int64_t)k * N);
+        double g[3][3];
+        const float* src = flip ? w + ((int64_t)k * cin + nidx) * 9 : w + ((int64_t)nidx * cin + k) * 9;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) g[i][j] = flip ? src[(2 - i) * 3 + (2 - j)] : src[i * 3 + j];
+        double gg[6][3];  // G g
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) gg[a][j] = Gm[a][0] * g[0][j] + Gm[a][1] * g[1][j] + Gm[a][2] * g[2][j];
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int b = 0; b < 6; ++b) {
+                const double u = gg[a][0] * Gm[b][0] + gg[a][1] * Gm[b][1] + gg[a][2] * Gm[b][2];
+                const int xi = 6 * b + a;
+                uw[(((int64_t)k * NXQ + (xi >> 2)) * N + nidx) * 4 + (xi & 3)] = (float)u;
+            }
+    }
+}
+
+template <int CG, int TG, int SM, int EK>
+void launch_w4(const Wino4Params& p, int64_t items, hipStream_t st) {
+    hipLaunchKernelGGL((wino4_kernel<CG, TG, SM, EK>), dim3((unsigned)items), dim3(512), 0, st, p);
+}
+
+template <int SM, int EK>
+void launch_w4_cfg(int cg, const Wino4Params& p, int64_t items, hipStream_t st) {
+    if (cg == 4) launch_w4<4, 2, SM, EK>(p, items, st);
+    else launch_w4<2, 4, SM, EK>(p, items, st);
+}
+
+template <int EK>
+void launch_w4_s(bool has_s, int cg, const Wino4Params& p, int64_t items, hipStream_t st) {
+    if (has_s) launch_w4_cfg<1, EK>(cg, p, items, st);
+    else launch_w4_cfg<2, EK>(cg, p, items, st);
+}
+
+// channel groups per work item: 4 (64 output channels x 32 tiles) where cout allows, else 2 (32 x 64)
+int w4_cg(int cout, int h, int w) {
+    if (w % 64 || w < 64) return 0;
+    if (cout % 64 == 0 && h % 8 == 0) return 4;
+    if (cout % 32 == 0 && h % 16 == 0) return 2;
+    return 0;
+}
+
+}  // namespace
+
+SMC_API int smc_conv3x3_wino4_supported(int n, int cin, int cout, int h, int w) {
+    if (n < 1 || cin < W4K || cin % W4K) return 0;
+    if ((int64_t)n * cin * h * w * 4 >= (1LL << 31)) return 0;  // raw buffer offsets are 32-bit
+    if ((int64_t)cin * 36 * cout * 4 >= (1LL << 31)) return 0;
+    return w4_cg(cout, h, w) != 0;
+}
+
+SMC_API int smc_wino4_weights_f32(const float* w, int cout, int cin, int flip, float* uw, void* stream) {
+    SMC_CHECK(w && uw && cout >= 1 && cin >= 1, "smc_wino4_weights_f32: bad arguments");
+    SMC_CHECK((reinterpret_cast<uintptr_t>(uw) & 15) == 0, "smc_wino4_weights_f32: uw must be 16-B aligned");
+    const int64_t total = (int64_t)cout * cin;
+    hipLaunchKernelGGL(wino4_weights_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(total, 256), 4096)),
+                       dim3(256), 0, smc::as_stream(stream), w, cout, cin, flip, uw);
+    return smc::check_launch("smc_wino4_weights_f32");
+}
+
+SMC_API int smc_conv3x3_wino4_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
+                                  const float* s_in, const smc_conv_epilogue* epi, void* stream) {
+    SMC_CHECK(x && y && uw, "smc_conv3x3_wino4_f32: null pointer");
+    if (!smc_conv3x3_wino4_supported(n, cin, cout, h, w)) {
+        smc::set_error("smc_conv3x3_wino4_f32: no Winograd F(4x4) kernel for n=%d cin=%d cout=%d %dx%d", n, cin, cout,
+                       h, w);
+        return SMC_ERR_UNSUPPORTED;
+    }
+    SMC_CHECK((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(uw) & 15) == 0,
+              "smc_conv3x3_wino4_f32: x / y / uw must be 16-B aligned");
+    smc_conv_epilogue e{};
+    e.mode = SMC_EPI_STORE; e.act = SMC_ACT_LINEAR; e.gain = 1.f; e.clamp = -1.f;
+    if (epi) e = *epi;
+    SMC_CHECK(e.mode >= SMC_EPI_STORE && e.mode <= SMC_EPI_AFFINE, "smc_conv3x3_wino4_f32: bad epilogue mode %d", e.mode);
+    SMC_CHECK((e.mode != SMC_EPI_PRELU && e.mode != SMC_EPI_PRELU_GRAD) || e.alpha_c,
+              "smc_conv3x3_wino4_f32: PReLU epilogue needs alpha_c");
+    SMC_CHECK(e.mode != SMC_EPI_PRELU_GRAD || e.act_ref, "smc_conv3x3_wino4_f32: PRELU_GRAD needs act_ref");
+    SMC_CHECK(!e.u_save || (reinterpret_cast<uintptr_t>(e.u_save) & 15) == 0, "smc_conv3x3_wino4_f32: u_save alignment");
+    SMC_CHECK(!e.noise || ((reinterpret_cast<uintptr_t>(e.noise) & 15) == 0 && e.noise_nstride % 4 == 0),
+              "smc_conv3x3_wino4_f32: noise must be 16-B aligned");
+    Wino4Params p{};
+    p.x = x; p.n = n; p.cin = cin; p.h = h; p.w = w; p.y = y; p.cout = cout; p.uw = uw; p.s = s_in;
+    p.mode = e.mode; p.d = e.d; p.noise = e.noise; p.noise_nstride = e.noise_nstride;
+    p.noise_strength = e.noise_strength; p.bias = e.bias; p.act = e.act; p.alpha = e.alpha; p.gain = e.gain;
+    p.clamp = e.clamp; p.u_save = e.u_save;
+    p.ext = smc::epi_ext(epi);
+    const int cg = w4_cg(cout, h, w);
+    const int tg = 8 / cg;
+    p.gx = w / 64;
+    p.gy = h / (4 * tg);
+    p.ntn = cout / (16 * cg);
+    const int64_t items = (int64_t)n * p.gx * p.gy * p.ntn;
+    SMC_CHECK(items < (1LL << 31), "smc_conv3x3_wino4_f32: grid too large");
+    hipStream_t st = smc::as_stream(stream);
+    const bool modact_plain = p.mode == SMC_EPI_MODACT && !p.ext.residual;
+    if (modact_plain && p.act == SMC_ACT_LRELU && p.alpha >= 0.f && p.alpha <= 1.f && p.clamp >= 0.f)
+        launch_w4_s<1>(s_in != nullptr, cg, p, items, st);
+    else if (modact_plain && p.act == SMC_ACT_LINEAR && p.clamp < 0.f)
+        launch_w4_s<2>(s_in != nullptr, cg, p, items, st);
+    else
+        launch_w4_s<0>(s_in != nullptr, cg, p, items, st);
+    return smc::check_launch("smc_conv3x3_wino4_f32");
+}

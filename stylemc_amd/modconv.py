@@ -65,6 +65,7 @@ class PackedConv:
             self.bwd_taps = [(ky, kx) for ky, kx in taps]  # stride-2 gather over dT
         self._cache = {}
         self._wino = {}
+        self._wino4 = {}
 
     def wino_weights(self, flip):
         """Winograd F(2x2, 3x3) transformed taps (smc_wino_weights_f32) of the 3x3 'same' conv, built once on the
@@ -79,6 +80,18 @@ class PackedConv:
             torch.cuda.current_stream(w.device).synchronize()
             self._wino[flip] = uw
         return self._wino[flip]
+
+    def wino4_weights(self, flip):
+        """Winograd F(4x4, 3x3) transformed taps (smc_wino4_weights_f32, 36 per channel pair), same contract as
+        wino_weights."""
+        if flip not in self._wino4:
+            W = self.wk_bwd
+            w = W.reshape(3, 3, self.cout, self.cin).permute(2, 3, 0, 1).contiguous()
+            uw = torch.empty(36 * self.cin * self.cout, device=w.device, dtype=torch.float32)
+            _hip.call("smc_wino4_weights_f32", w.data_ptr(), self.cout, self.cin, flip, uw.data_ptr(), _hip.stream())
+            torch.cuda.current_stream(w.device).synchronize()
+            self._wino4[flip] = uw
+        return self._wino4[flip]
 
     def fwd_phases(self, h, w):
         key = ("f", h, w)
@@ -141,6 +154,27 @@ def wino(x, y, uw, cin, cout, s=None, epi=None, alg_flops=0.0, alg_bytes=0):
               ctypes.byref(epi) if epi is not None else None, _hip.stream())
     if tok is not None:
         tm.finish(tok)
+
+
+def wino4_ok(n, cin, cout, h, w):
+    return WINOGRAD and bool(_hip.load().smc_conv3x3_wino4_supported(n, cin, cout, h, w))
+
+
+def wino4(x, y, uw, cin, cout, s=None, epi=None, alg_flops=0.0, alg_bytes=0):
+    """One smc_conv3x3_wino4_f32 launch (F(4x4, 3x3)).  alg_flops: the MFMA FLOPs it executes (36 / 144 of the
+    direct conv's; the timer also records the direct-equivalent count)."""
+    n, _, h, w = x.shape
+    tm = _hip.timer()
+    tok = tm.wrap(alg_flops, alg_bytes, kind="wino", equiv_flops=alg_flops * 4) if tm is not None else None
+    _hip.call("smc_conv3x3_wino4_f32", x.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(), _hip.ptr(s),
+              ctypes.byref(epi) if epi is not None else None, _hip.stream())
+    if tok is not None:
+        tm.finish(tok)
+
+
+def wino4_flops(n, cin, cout, h, w):
+    """MFMA FLOPs of one F(4x4, 3x3) launch: 36 multiplies per 4x4 tile and channel pair."""
+    return 2.0 * n * cin * cout * (h // 4) * (w // 4) * 36
 
 
 def wino_flops(n, cin, cout, h, w):

@@ -1,4 +1,4 @@
-"""Winograd F(2x2, 3x3) vs the direct implicit GEMM on the synthesis conv1 shapes (FFHQ-1024, batch 4).
+"""Winograd F(2x2, 3x3) and F(4x4, 3x3) vs the direct implicit GEMM on the synthesis conv1 shapes (FFHQ-1024, batch 4).
 
     python tools/bench_wino.py [--batch 4] [--reps 10]
 Per shape: us per launch of each path, the direct-equivalent TFLOP/s (dense 3x3 MACs x 2 / time) and the Winograd
@@ -36,7 +36,7 @@ def main():
     args = ap.parse_args()
     build.build(verbose=False)
     n, dev = args.batch, "cuda"
-    tot = {"direct": 0.0, "wino": 0.0}
+    tot = {"direct": 0.0, "wino": 0.0, "wino4": 0.0}
     for r in [32, 64, 128, 256, 512, 1024]:
         c = min(32768 // r, 512)
         W = torch.randn(c, c, 3, 3, device=dev) / (3 * c ** 0.5)
@@ -47,6 +47,9 @@ def main():
         phases, nph, _, _ = P.fwd_phases(r, r)
         bph, bnph = P.bwd_phases(r, r)
         uf, ub = P.wino_weights(0), P.wino_weights(1)
+        has4 = modconv.wino4_ok(n, c, c, r, r)
+        if has4:
+            uf4, ub4 = P.wino4_weights(0), P.wino4_weights(1)
         st = modconv._epilogue(_hip.EPI_STORE)
         runs = {
             ("fwd", "direct"): lambda: modconv.gemm(x, y, phases, nph, c, c, s=s, epi=st),
@@ -54,8 +57,12 @@ def main():
             ("bwd", "direct"): lambda: modconv.gemm(x, y, bph, bnph, c, c, epi=st),
             ("bwd", "wino"): lambda: modconv.wino(x, y, ub, c, c, epi=st),
         }
+        if has4:
+            runs[("fwd", "wino4")] = lambda: modconv.wino4(x, y, uf4, c, c, s=s, epi=st)
+            runs[("bwd", "wino4")] = lambda: modconv.wino4(x, y, ub4, c, c, epi=st)
         flops = modconv.conv_flops(n, c, c, r, r, 9)
         wfl = modconv.wino_flops(n, c, c, r, r)
+        wfl4 = modconv.wino4_flops(n, c, c, r, r)
         for kind in ("fwd", "bwd"):
             td = timeit(runs[(kind, "direct")], args.reps)
             tw = timeit(runs[(kind, "wino")], args.reps)
@@ -64,8 +71,15 @@ def main():
             print(f"r={r:5d} c={c:4d} {kind}: direct {td * 1e6:8.1f} us ({flops / td / 1e12:6.1f} TF/s, "
                   f"{flops / td / PEAK:.3f})  wino {tw * 1e6:8.1f} us (eq {flops / tw / 1e12:6.1f} TF/s, "
                   f"MFMA frac {wfl / tw / PEAK:.3f})  speedup {td / tw:.2f}x", flush=True)
+            if has4:
+                t4 = timeit(runs[(kind, "wino4")], args.reps)
+                tot["wino4"] += t4
+                print(f"            {kind}: wino4 {t4 * 1e6:8.1f} us (eq {flops / t4 / 1e12:6.1f} TF/s, "
+                      f"MFMA frac {wfl4 / t4 / PEAK:.3f})  vs wino {tw / t4:.2f}x", flush=True)
+            else:
+                tot["wino4"] += tw
     print(f"total: direct {tot['direct'] * 1e3:.3f} ms, wino {tot['wino'] * 1e3:.3f} ms, "
-          f"speedup {tot['direct'] / tot['wino']:.2f}x")
+          f"speedup {tot['direct'] / tot['wino']:.2f}x; best-of wino4/wino {tot['wino4'] * 1e3:.3f} ms")
 
 
 if __name__ == "__main__":

@@ -1,5 +1,6 @@
 """Run one Winograd conv shape repeatedly (for rocprofv3 PMC passes).
-    python tools/wino_one.py KIND R [reps]     KIND in fwd bwd (the conv1 of resolution R, batch 4)"""
+    python tools/wino_one.py KIND R [reps]     KIND in fwd bwd fwd4 bwd4 (the conv1 of resolution R, batch 4;
+                                               fwd4 / bwd4: the F(4x4) kernel)"""
 import os
 import sys
 
@@ -18,9 +19,11 @@ P = modconv.PackedConv(W, 1)
 x = torch.randn(n, c, r, r, device=dev)
 s = torch.rand(n, c, device=dev) + 0.5
 y = torch.empty_like(x)
-uw = P.wino_weights(0 if kind == "fwd" else 1)
+f4 = kind.endswith("4")
+flip = 0 if kind.startswith("fwd") else 1
+uw = P.wino4_weights(flip) if f4 else P.wino_weights(flip)
 st = modconv._epilogue(_hip.EPI_STORE)
 for _ in range(reps):
-    modconv.wino(x, y, uw, c, c, s=s if kind == "fwd" else None, epi=st)
+    (modconv.wino4 if f4 else modconv.wino)(x, y, uw, c, c, s=s if flip == 0 else None, epi=st)
 torch.cuda.synchronize()
 print("done", kind, r)
