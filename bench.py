@@ -15,9 +15,10 @@ image per seed), seeds counted exactly (the batch picker 
 last batch of the 129 seeds).
 
 roofline: the dominant kernel family, the synthesis convs (every smc_conv3x3_wino_f32 / smc_conv_gemm_f32 launch
-from modconv.py: ``wino_kernel`` for the 3x3 'same' convs, ``conv_gemm_lds_kernel`` / ``conv_row_kernel`` /
+from modconv.py: ``wino4_kernel`` / ``wino_kernel`` for the 3x3 'same' convs, ``conv_gemm_lds_kernel`` / ``conv_row_kernel`` /
 ``convt_lds_kernel`` ... for the rest): the MFMA FLOPs of each launch's algorithm (dense MACs x 2 for the direct
-kernels; 16 multiplies per 2x2 tile and channel pair for Winograd, reported beside the
+kernels; 16 / 36 multiplies per 2x2 / 4x4 tile and channel pair for Winograd F(2x2) / F(4x4),
+reported beside the
 direct-equivalent rate) / its duration, timed with HIP events around every launch during --roofline-steps extra steps run right
 after the timed region with the original-image branch serialised onto the main stream (in the timed
 region that branch runs on a second stream, and a launch's event interval would include CU time
@@ -303,8 +304,12 @@ def main():
                     "direct_equiv_tflops": round(d["equiv_flops"] / d["seconds"] / 1e12, 3) if d["seconds"] > 0 else 0.0}
 
         kinds = {
-            "wino": ("Winograd F(2x2,3x3) 3x3 'same' convs (conv1 fwd + data grad); FLOPs = its 16 multiplies "
-                            "per 2x2 tile and channel pair (4/9 of the direct conv's)"),
+            "wino": ("Winograd F(2x2,3x3) 3x3 'same' convs with a 32/64-channel input (conv1 fwd + data grad at "
+                     "r = 32, 512, 1024); FLOPs = its 16 multiplies per 2x2 tile and channel pair (4/9 of the direct "
+                     "conv's)"),
+            "wino4": ("Winograd F(4x4,3x3) 3x3 'same' convs with >= 128 input channels (conv1 fwd + data grad at "
+                      "r = 64..256); FLOPs = its 36 multiplies per 4x4 tile and channel pair (1/4 of the direct "
+                      "conv's)"),
             "direct": ("direct implicit-GEMM kernels (conv_gemm_lds / conv_row / convt_lds ...: transposed conv0, "
                        "its stride-2 data grad, the < 32-px layers); FLOPs = dense MACs x 2"),
         }
@@ -315,13 +320,15 @@ def main():
         roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                     "traffic_source": traffic_src,
-                    "frac_basis": "executed MFMA FLOPs (Winograd: its 16 multiplies per 2x2 tile and channel pair)",
+                    "frac_basis": "executed MFMA FLOPs (Winograd: its 16 / 36 multiplies per 2x2 / 4x4 tile and "
+                                  "channel pair)",
                     "dense_equiv_frac": round(equiv / FP32_MFMA_PEAK_TFLOPS, 4),
                     "dense_equiv_basis": "SURVEY 8(d) dense conv MACs x 2 per second / fp32 MFMA peak (above 1 is "
-                                         "possible: Winograd executes 4/9 of the dense multiplies)",
+                                         "possible: Winograd executes 4/9 (F(2x2)) or 1/4 (F(4x4)) of the dense "
+                                         "multiplies)",
                     "dominant_kernel": ({"part": dom, "frac": parts[dom]["frac"],
                                          "ms_per_step": parts[dom]["ms_per_step"]} if dom else None),
-                    "kernel": "synthesis conv family (wino_kernel + the direct implicit-GEMM kernels)",
+                    "kernel": "synthesis conv family (wino_kernel + wino4_kernel + the direct implicit-GEMM kernels)",
                     "launches": s["launches"],
                     "avg_launch_us": round(1e6 * s["seconds"] / max(s["launches"], 1), 2),
                     "alg_gflop_per_launch": round(s["flops"] / max(s["launches"], 1) / 1e9, 3),

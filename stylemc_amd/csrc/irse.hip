@@ -60,115 +60,143 @@ __global__ __launch_bounds__(256) void plane_dot_kernel(const float* a, const fl
     if (lane == 0) out[pl] = s * scale;
 }
 
-// Squeeze-and-excite excitation, one workgroup of 16 waves per sample.  The chain is latency-bound (a few KB
-// of weights per sample, n <= 8 workgroups): the FC rows are one wave each, unrolled over their 64-lane
-// strides, and the operands that do not depend on an earlier phase are loaded up front.  The plane sums come
-// from plane_dot_kernel: summed inside this kernel instead (8..16 planes per wave) the 14x14 / 7x7 stages
-// measured 10.5 / 17 us forward against 4.8 + 4.8 / 4.8 + 10 as two launches (tools/prof_irse.py).
-constexpr int kSeThreads = 1024;
-constexpr int kSeWaves = kSeThreads / 64;
-
-// h = relu(W1 m), g = sigmoid(W2 h), m = mean_hw(r) from plane_dot_kernel.
-__global__ __launch_bounds__(kSeThreads) void se_fwd_kernel(const float* m, const float* w1, const float* w2, float* h,
-                                                            float* g, int C, int hid) {
-    extern __shared__ float sm[];
-    float* ms = sm;
-    float* hs = sm + C;
-    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int c = tid; c < C; c += kSeThreads) ms[c] = m[(int64_t)n * C + c];
-    __syncthreads();
-    for (int j = wave; j < hid; j += kSeWaves) {
-        float s = 0.f;
-#pragma unroll 8
-        for (int c = lane; c < C; c += 64) s += w1[(int64_t)j * C + c] * ms[c];
-        s = wsum(s);
-        if (lane == 0) {
-            const float v = s > 0.f ? s : 0.f;
-            hs[j] = v;
-            h[(int64_t)n * hid + j] = v;
-        }
-    }
-    __syncthreads();
-    for (int c = tid; c < C; c += kSeThreads) {
-        float s = 0.f;
-#pragma unroll 8
-        for (int j = 0; j < hid; ++j) s += w2[(int64_t)c * hid + j] * hs[j];
-        g[(int64_t)n * C + c] = 1.f / (1.f + expf(-s));
-    }
-}
-
-// SE backward per sample: dg = sum_hw dout * r from plane_dot_kernel; dz = dg * g(1-g); dh = (h > 0) * W2^T dz;
-// dm = W1^T dh * inv_hw.
-__global__ __launch_bounds__(kSeThreads) void se_bwd_kernel(const float* dg, const float* g, const float* h,
-                                                            const float* w1, const float* w2, float* dm, int C, int hid,
-                                                            float inv_hw) {
-    extern __shared__ float sm[];
-    float* dz = sm;
-    float* dh = sm + C;
-    float* hs = sm + C + hid;
-    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int j = tid; j < hid; j += kSeThreads) hs[j] = h[(int64_t)n * hid + j];
-    for (int c = tid; c < C; c += kSeThreads) {
-        const float gv = g[(int64_t)n * C + c];
-        dz[c] = dg[(int64_t)n * C + c] * gv * (1.f - gv);
-    }
-    __syncthreads();
-    for (int j = wave; j < hid; j += kSeWaves) {
-        float s = 0.f;
-#pragma unroll 8
-        for (int c = lane; c < C; c += 64) s += w2[(int64_t)c * hid + j] * dz[c];
-        s = wsum(s);
-        if (lane == 0) dh[j] = hs[j] > 0.f ? s : 0.f;
-    }
-    __syncthreads();
-    for (int c = tid; c < C; c += kSeThreads) {
-        float s = 0.f;
-#pragma unroll 8
-        for (int j = 0; j < hid; ++j) s += w1[(int64_t)j * C + c] * dh[j];
-        dm[(int64_t)n * C + c] = s * inv_hw;
-    }
-}
-
-// out = r * g[n,c] + shortcut; shortcut = sc[idx] (conv path) or x[n, c, s*y, s*x] (MaxPool2d(1, s));
-// xbn (optional) = out * a[c] + b[c]  (BN1 of the next unit).
-__global__ __launch_bounds__(256) void se_combine_kernel(const float* r, const float* g, const float* sc,
-                                                         const float* x, int s, int in_h, int in_w, float* out,
-                                                         float* xbn, const float* a, const float* b, int C, int oh,
-                                                         int ow, int64_t total) {
-    const int64_t ohw = (int64_t)oh * ow;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t nc = i / ohw;
-        const int p = (int)(i - nc * ohw);
-        float v = r[i] * g[nc];
-        if (sc) {
-            v += sc[i];
-        } else {
-            const int yy = p / ow, xx = p - yy * ow;
-            v += x[nc * ((int64_t)in_h * in_w) + (int64_t)(s * yy) * in_w + s * xx];
-        }
-        out[i] = v;
-        if (xbn) {
-            const int c = (int)(nc % C);
-            xbn[i] = v * a[c] + b[c];
-        }
-    }
-}
-
-// dr = dout * g[n,c] + dm[n,c]
-__global__ __launch_bounds__(256) void se_dr_kernel(const float* dout, const float* g, const float* dm, float* dr,
-                                                    int64_t hw, int64_t total) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t nc = i / hw;
-        dr[i] = dout[i] * g[nc] + dm[nc];
-    }
-}
-
+// Squeeze-and-excite.  The chain is latency-bound (a few KB of weights per sample, n <= 8 samples): the plane sums
+// come from plane_dot_kernel (summed inside the excitation kernel instead, 8..16 planes per wave, the 14x14 / 7x7
+// stages measured 10.5 / 17 us forward against 4.8 + 4.8 / 4.8 + 10 as two launches, tools/prof_irse.py); the
+// excitation MLP is recomputed per channel block inside the combine / dr kernels below (it replaced a separate
+// excitation launch per unit and direction).
 // y = x * a[c] + b[c]
 __global__ __launch_bounds__(256) void channel_affine_kernel(const float* x, const float* a, const float* b, float* y,
                                                              int C, int64_t hw, int64_t total) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         const int c = (int)((i / hw) % C);
         y[i] = x[i] * a[c] + b[c];
+    }
+}
+
+// SE excitation + combine (forward), one workgroup per (sample n, block of kSeCpb channels).  Each workgroup
+// recomputes the sample's hidden layer h = relu(W1 m) (hid C-dots: a few KFLOP, cheaper than the launch of a separate
+// excitation kernel on this latency-bound chain), then g = sigmoid(W2 h) for its channels, and applies
+// out = r * g + shortcut (shortcut = sc (conv path) or x[n, c, s*y, s*x] (MaxPool2d(1, s))) and, optionally,
+// xbn = out * a[c] + b[c] (BN1 of the next unit).  h (channel block 0) and g are stored for the backward.
+constexpr int kSeCpb = 16;
+// pixel-range split of a plane for the SE kernels: at most 256 pixels (one per thread) of each of the kSeCpb channels
+// per workgroup
+inline unsigned se_zsplit(int64_t hw) { return (unsigned)std::max<int64_t>(1, smc::ceil_div(hw, 256)); }
+__global__ __launch_bounds__(256) void se_fwd_combine_kernel(const float* m, const float* w1, const float* w2,
+                                                             float* hout, float* gout, int C, int hid, const float* r,
+                                                             const float* sc, const float* x, int s, int in_h,
+                                                             int in_w, float* out, float* xbn, const float* a,
+                                                             const float* b, int oh, int ow) {
+    extern __shared__ float sm[];
+    float* ms = sm;         // [C]
+    float* hs = sm + C;     // [hid]
+    float* gs = hs + hid;   // [kSeCpb]
+    float* as = gs + kSeCpb;  // [kSeCpb] BN1 scale / shift of the next unit (xbn)
+    float* bs = as + kSeCpb;
+    const int n = blockIdx.x, c0 = blockIdx.y * kSeCpb;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // this thread's pixel (se_zsplit: at most 256 pixels of a plane per workgroup), its kSeCpb channels of r and of
+    // the shortcut loaded first: their round trips overlap the excitation MLP's
+    const int ohw = oh * ow;
+    const int chunk = (ohw + gridDim.z - 1) / gridDim.z;
+    const int p = blockIdx.z * chunk + tid;
+    const bool live = tid < chunk && p < ohw;
+    const int pc = live ? p : 0;
+    const int64_t nb = (int64_t)n * C + c0;
+    float rv[kSeCpb], sv[kSeCpb];
+    {
+        int64_t xo = 0;
+        if (!sc) {
+            const int yy = pc / ow, xx = pc - yy * ow;
+            xo = (int64_t)(s * yy) * in_w + s * xx;
+        }
+#pragma unroll
+        for (int cl = 0; cl < kSeCpb; ++cl) {
+            const int64_t i = (nb + cl) * ohw + pc;
+            rv[cl] = r[i];
+            sv[cl] = sc ? sc[i] : x[(nb + cl) * ((int64_t)in_h * in_w) + xo];
+        }
+    }
+    for (int c = tid; c < C; c += 256) ms[c] = m[(int64_t)n * C + c];
+    __syncthreads();
+    for (int j = wave; j < hid; j += 4) {
+        float t = 0.f;
+#pragma unroll 8
+        for (int c = lane; c < C; c += 64) t += w1[(int64_t)j * C + c] * ms[c];
+        t = wsum(t);
+        if (lane == 0) hs[j] = t > 0.f ? t : 0.f;
+    }
+    __syncthreads();
+    if (tid < kSeCpb) {
+        const int c = c0 + tid;
+        float t = 0.f;
+#pragma unroll 8
+        for (int j = 0; j < hid; ++j) t += w2[(int64_t)c * hid + j] * hs[j];
+        as[tid] = xbn ? a[c] : 0.f;
+        bs[tid] = xbn ? b[c] : 0.f;
+        gs[tid] = 1.f / (1.f + expf(-t));
+    }
+    __syncthreads();
+    // (the stores after every load: a load issued behind a store waits for its round trip)
+    if (tid < kSeCpb) gout[(int64_t)n * C + c0 + tid] = gs[tid];
+    if (blockIdx.y == 0 && blockIdx.z == 0 && tid < hid) hout[(int64_t)n * hid + tid] = hs[tid];
+    if (live) {
+#pragma unroll
+        for (int cl = 0; cl < kSeCpb; ++cl) {
+            const int64_t i = (nb + cl) * ohw + p;
+            const float o = rv[cl] * gs[cl] + sv[cl];
+            out[i] = o;
+            if (xbn) xbn[i] = o * as[cl] + bs[cl];
+        }
+    }
+}
+
+// SE backward + dr (one workgroup per (sample, channel block), like se_fwd_combine_kernel): from dg = sum_hw dout * r
+// (plane_dot_kernel) every workgroup recomputes dz = dg g (1 - g) and dh = (h > 0) W2^T dz for its sample, then
+// dm = W1^T dh * inv_hw for its channels and dr = dout * g + dm.
+__global__ __launch_bounds__(256) void se_bwd_dr_kernel(const float* dg, const float* g, const float* h,
+                                                        const float* w1, const float* w2, int C, int hid, float inv_hw,
+                                                        const float* dout, float* dr, int64_t hw) {
+    extern __shared__ float sm[];
+    float* dz = sm;          // [C]
+    float* dh = sm + C;      // [hid]
+    float* dms = dh + hid;   // [kSeCpb]
+    float* gsb = dms + kSeCpb;  // [kSeCpb]
+    const int n = blockIdx.x, c0 = blockIdx.y * kSeCpb;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int chunk = (int)((hw + gridDim.z - 1) / gridDim.z);
+    const int p = blockIdx.z * chunk + tid;
+    const bool live = tid < chunk && p < hw;
+    const int64_t nb = (int64_t)n * C + c0;
+    float dv[kSeCpb];  // this thread's pixel of dout, loaded before the SE chain
+#pragma unroll
+    for (int cl = 0; cl < kSeCpb; ++cl) dv[cl] = dout[(nb + cl) * hw + (live ? p : 0)];
+    for (int c = tid; c < C; c += 256) {
+        const float gv = g[(int64_t)n * C + c];
+        dz[c] = dg[(int64_t)n * C + c] * gv * (1.f - gv);
+    }
+    __syncthreads();
+    for (int j = wave; j < hid; j += 4) {
+        float t = 0.f;
+#pragma unroll 8
+        for (int c = lane; c < C; c += 64) t += w2[(int64_t)c * hid + j] * dz[c];
+        t = wsum(t);
+        if (lane == 0) dh[j] = h[(int64_t)n * hid + j] > 0.f ? t : 0.f;
+    }
+    __syncthreads();
+    if (tid < kSeCpb) {
+        const int c = c0 + tid;
+        float t = 0.f;
+#pragma unroll 8
+        for (int j = 0; j < hid; ++j) t += w1[(int64_t)j * C + c] * dh[j];
+        dms[tid] = t * inv_hw;
+        gsb[tid] = g[(int64_t)n * C + c];
+    }
+    __syncthreads();
+    if (live) {
+#pragma unroll
+        for (int cl = 0; cl < kSeCpb; ++cl) dr[(nb + cl) * hw + p] = dv[cl] * gsb[cl] + dms[cl];
     }
 }
 
@@ -307,6 +335,8 @@ int net_validate(const smc_irse_net* net, int n) {
         SMC_CHECK(u.stride == 1 || u.stride == 2, "smc_irse: unit %d stride %d", k, u.stride);
         SMC_CHECK(u.in_h % u.stride == 0 && u.in_w % u.stride == 0, "smc_irse: unit %d odd size", k);
         SMC_CHECK(u.se_hidden >= 1 && u.se_w1 && u.se_w2 && u.bn1_a && u.bn2_a && u.prelu, "smc_irse: unit %d", k);
+        SMC_CHECK(u.depth % kSeCpb == 0, "smc_irse: unit %d depth %d not a multiple of %d", k, u.depth, kSeCpb);
+        SMC_CHECK(u.se_hidden <= 256, "smc_irse: unit %d SE hidden width %d > 256", k, u.se_hidden);
         SMC_CHECK(u.sc_conv || u.cin == u.depth, "smc_irse: unit %d identity shortcut needs cin == depth", k);
         SMC_CHECK(u.c2_bwd_nphases == (u.stride == 2 ? 4 : 1), "smc_irse: unit %d adjoint phases", k);
     }
@@ -399,9 +429,6 @@ SMC_API int smc_irse_forward_f32(const smc_irse_net* net, const float* img, int 
         const int64_t planes = (int64_t)n * u.depth;
         hipLaunchKernelGGL(plane_dot_kernel<false>, dim3((unsigned)smc::ceil_div(planes, 4)), dim3(256), 0, st, r,
                            (const float*)nullptr, w.m, planes, (int)ohw, 1.f / (float)ohw);
-        hipLaunchKernelGGL(se_fwd_kernel, dim3(n), dim3(kSeThreads), sizeof(float) * (u.depth + u.se_hidden), st, w.m,
-                           u.se_w1, u.se_w2, hbuf, gbuf, u.depth, u.se_hidden);
-        SMC_TRY(smc::check_launch("irse se"));
         // shortcut
         const float* sc = nullptr;
         if (u.sc_conv) {
@@ -411,14 +438,14 @@ SMC_API int smc_irse_forward_f32(const smc_irse_net* net, const float* img, int 
             SMC_TRY(conv(x, u.cin, u.in_h, u.in_w, w.sc, u.depth, oh, ow, &u.sc_fwd, 1, e));
             sc = w.sc;
         }
-        // out = r * g + shortcut (+ BN1 of the next unit)
+        // g = sigmoid(W2 relu(W1 m)); out = r * g + shortcut (+ BN1 of the next unit): one fused launch
         float* out = x == w.xa ? w.xb : w.xa;
         const bool next = k + 1 < net->n_units;
-        tot = planes * ohw;
-        hipLaunchKernelGGL(se_combine_kernel, dim3(ew_grid(tot)), dim3(256), 0, st, r, gbuf, sc, x, u.stride,
-                           u.in_h, u.in_w, out, next ? w.xbn : nullptr, next ? net->units[k + 1].bn1_a : nullptr,
-                           next ? net->units[k + 1].bn1_b : nullptr, u.depth, oh, ow, tot);
-        SMC_TRY(smc::check_launch("irse combine"));
+        hipLaunchKernelGGL(se_fwd_combine_kernel, dim3(n, u.depth / kSeCpb, se_zsplit(ohw)), dim3(256),
+                           sizeof(float) * (u.depth + u.se_hidden + 3 * kSeCpb), st, w.m, u.se_w1, u.se_w2, hbuf, gbuf,
+                           u.depth, u.se_hidden, r, sc, x, u.stride, u.in_h, u.in_w, out, next ? w.xbn : nullptr,
+                           next ? net->units[k + 1].bn1_a : nullptr, next ? net->units[k + 1].bn1_b : nullptr, oh, ow);
+        SMC_TRY(smc::check_launch("irse se + combine"));
         x = out;
     }
     // output layer: folded BN2d + Linear + BN1d
@@ -460,10 +487,9 @@ SMC_API int smc_irse_backward_f32(const smc_irse_net* net, const float* dfeat, i
         // SE + combine backward: dg = sum_hw dout * r; dm = SE chain; dr = dout * g + dm
         hipLaunchKernelGGL(plane_dot_kernel<true>, dim3((unsigned)smc::ceil_div(planes, 4)), dim3(256), 0, st, dout,
                            us[k].r, w.m, planes, (int)ohw, 1.f);
-        hipLaunchKernelGGL(se_bwd_kernel, dim3(n), dim3(kSeThreads), sizeof(float) * (u.depth + 2 * u.se_hidden), st,
-                           w.m, us[k].g, us[k].h, u.se_w1, u.se_w2, w.dm, u.depth, u.se_hidden, 1.f / (float)ohw);
-        const int64_t tot = planes * ohw;
-        hipLaunchKernelGGL(se_dr_kernel, dim3(ew_grid(tot)), dim3(256), 0, st, dout, us[k].g, w.dm, w.r, ohw, tot);
+        hipLaunchKernelGGL(se_bwd_dr_kernel, dim3(n, u.depth / kSeCpb, se_zsplit(ohw)), dim3(256),
+                           sizeof(float) * (u.depth + u.se_hidden + 2 * kSeCpb), st, w.m, us[k].g, us[k].h, u.se_w1,
+                           u.se_w2, u.depth, u.se_hidden, 1.f / (float)ohw, dout, w.r, ohw);
         SMC_TRY(smc::check_launch("irse se bwd"));
         // du1 = PReLU'(u1) * conv2^T(dr)   (BN2 scale folded into the adjoint weights)
         smc_conv_epilogue e = epi_mode(SMC_EPI_PRELU_GRAD);

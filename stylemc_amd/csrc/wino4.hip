@@ -12,20 +12,16 @@
 //   A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
 // Index xi = 6 b + a for the element (row a, column b) of the 6x6 transform domain.
 //
-// Work decomposition (512 threads = 8 waves, one workgroup per CU, 2 waves per SIMD):
-//   * a work item is 16 CG output channels x 16 TG tiles (TG tile rows x 16 tile columns = 4 TG x 64 outputs of
-//     one image); wave w owns channel group w % CG and tile row w / CG: 16 channels x 16 tiles, all 36 xi = 36
-//     accumulators of the 16x16x4 MFMA (144 registers).  A lane holds one tile and 4 channels of each, so the 36
-//     M values of a (channel, tile) sit in one lane and the output transform + modconv epilogue are lane-local.
-//   * K steps of 4 input channels (the MFMA's k).  V is computed ONCE per workgroup and shared through LDS by the
-//     CG channel groups: per step, TG waves (alternating halves of the workgroup, so every SIMD carries the same
-//     transform load over two steps) each transform 64 patches (one per lane: 36 reads, 2 x 6 six-point
-//     transforms, x s[n, c], 9 ds_write_b128), the other waves only issue MFMAs.  The transform of step k + 1 runs
-//     under the MFMAs of step k.
-//   * Operands by DMA (buffer_load ... lds): the U slab [4][9][16 CG][4] one step ahead, the raw input rows of the
-//     block's (4 TG + 2) x 72 patch two steps ahead (16-B chunks from column 4 tx0 - 4; the buffer range check
-//     zero-fills the image border).  LDS: 2 x (U + patch + V) = 132 KiB (CG 4) / 150 KiB (CG 2); one barrier per
-//     step.
+// Work decomposition (one 768-thread workgroup per CU, roles below the W4Cfg definition):
+//   * a work item is 64 output channels x 32 tiles (2 tile rows x 16 tile columns = 8 x 64 outputs of one image);
+//     each of the 8 MFMA waves owns 16 channels x 16 tiles, all 36 xi = 36 accumulators of the 16x16x4 MFMA (144
+//     registers).  A lane holds one tile and 4 channels of each, so the 36 M values of a (channel, tile) sit in one
+//     lane and the output transform + modconv epilogue are lane-local.
+//   * K steps of 4 input channels (the MFMA's k).  V is computed ONCE per workgroup by two transform waves and shared
+//     through LDS by the 4 channel groups; two DMA waves stage the operands (buffer_load ... lds): the U slab
+//     [4][9][64][4] one step ahead, the raw input rows of the block's 10 x 72 patch two steps ahead (16-B chunks from
+//     column 4 tx0 - 4; the buffer range check zero-fills the image border).  LDS: 2 x (U + patch + V) = 132 KiB;
+//     one barrier per step.
 #include <algorithm>
 #include <type_traits>
 
@@ -59,7 +55,7 @@ struct Wino4Params {
     float* u_save;
     smc::EpiExt ext;
     int gx, gy;  // tile blocks per image along x / y
-    int ntn;     // output-channel blocks (cout / (16 CG))
+    int ntn;     // output-channel blocks (cout / 64)
 };
 
 template <int CG, int TG>
@@ -112,30 +108,36 @@ struct W4Item {
     int nn, ty0, tx0, o0;
 };
 
+// Wave roles (12 waves = 768 threads, 3 per SIMD, one workgroup per CU; the roles run concurrently, one s_barrier
+// per K step for all of them):
+//   waves 0-7   consumers: only MFMAs (A fragments from the U slot, B fragments from the V slot of step k) and, after
+//               the K loop, the output transform + epilogue.  Wave w owns channel group w % 4 and tile row w / 4.
+//   waves 8-9   transform: V(k + 1) from the patch of step k + 1 (64 patches each: 18 LDS reads, 2 x 6 six-point
+//               transforms, x s[n, c], 9 ds_write_b128).
+//   waves 10-11 DMA: U(k + 1) and the patch of step k + 2 into their LDS slots (24 LDS-DMAs each), then their wait.
+// Measured before the split (tools/probes/wino4_probe.hip, r = 64): with the transform and the DMAs issued by the MFMA
+// waves, removing the transform took a launch from 338 to 196 us and removing the DMAs to 250 us -- a wave that
+// serialises LDS reads, VALU and DMA issue between its own MFMAs starves the matrix pipe of its SIMD.
 // SM: style scale s[n, c] (1: present, 2: absent).  EK: epilogue body (1: MODACT lrelu + gain + clamp, 2: MODACT
 // linear, 0: any mode through smc::epi_y / epi_ext_apply).  PROBE (0 in the library; tools/probes/wino4_probe.hip)
-// removes pieces for timing: 1 the U DMAs after step 0, 2 the patch DMAs after step 1, 4 the transform, 8 the
-// per-step wait + barrier.
-template <int CG, int TG, int SM, int EK, int PROBE = 0>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+// removes pieces for timing: 1 the U DMAs after step 0, 2 the patch DMAs after step 1, 4 the transform after step 0.
+constexpr int W4_THREADS = 768;
+
+template <int SM, int EK, int PROBE = 0>
+__global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3)))
 void wino4_kernel(Wino4Params p) {
-    using C = W4Cfg<CG, TG>;
-    constexpr int OB = C::OB, TB = C::TB, ROWS = C::ROWS, SLAB = C::SLAB, STAGE = C::STAGE;
-    constexpr int UJ = C::UJ, PJ = C::PJ, UJW = C::UJW, PJW = C::PJW;
+    using C = W4Cfg<4, 2>;
+    constexpr int OB = C::OB, TB = C::TB, SLAB = C::SLAB, STAGE = C::STAGE, ROWS = C::ROWS;
+    constexpr int UJ = C::UJ, PJ = C::PJ;
     __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int cg = wave % CG, tg = wave / CG;
     const int H = p.h, W = p.w;
     const int64_t plane = (int64_t)H * W;
     const int nsteps = p.cin / W4K;
     const int total = p.n * p.gx * p.gy * p.ntn;
-    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * plane * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ursrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.uw, (short)0, p.cin * 36 * p.cout * 4, 0x00020000);
 
     const int v = blockIdx.x;
     if (v >= total) return;
@@ -149,156 +151,147 @@ void wino4_kernel(Wino4Params p) {
         const int per_img = p.gx * p.gy;
         it.nn = tgi / per_img;
         const int rem = tgi - it.nn * per_img;
-        it.ty0 = (rem / p.gx) * TG;
+        it.ty0 = (rem / p.gx) * 2;
         it.tx0 = (rem % p.gx) * 16;
         it.o0 = ob * OB;
     }
 
-    // per-lane DMA byte offsets of step 0 (a step adds a scalar offset)
-    // U: 16-B lane L = (wave + 8 j) 64 + lane = run * OB + o (run = c * 9 + xq); instruction j adds 512 / OB runs,
-    // a scalar offset
-    int pv[PJW];
-    const int uv0 = (((wave * 64 + lane) / OB) * p.cout + it.o0 + (wave * 64 + lane) % OB) * 16;
-    const int ujs = (512 / OB) * p.cout * 16;
+    if (wave >= 10) {
+        // ---- DMA waves: U instructions j = d, d + 2, ... (run j of the slab: 64 output channels x 16 B), patch
+        // instructions jj = d, d + 2, ... (16-B lane L = (c * ROWS + r) * PCH + ch)
+        constexpr int UPW = UJ / 2, PPW = (PJ + 1) / 2;
+        const int d = wave - 10;
+        const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * plane * 4), 0x00020000);
+        const __amdgpu_buffer_rsrc_t ursrc =
+            __builtin_amdgcn_make_buffer_rsrc((void*)p.uw, (short)0, p.cin * 36 * p.cout * 4, 0x00020000);
+        const int uv0 = (it.o0 + lane) * 16;
+        int pv[PPW];
 #pragma unroll
-    for (int jj = 0; jj < PJW; ++jj) {
-        const int L = (wave + 8 * jj) * 64 + lane;  // = (c * ROWS + r) * PCH + ch
-        const int c = L / (ROWS * PCH);
-        const int r2 = L - c * (ROWS * PCH);
-        const int r = r2 / PCH, ch = r2 - r * PCH;
-        const int gyy = 4 * it.ty0 - 1 + r, gxx = 4 * it.tx0 - 4 + 4 * ch;
-        const bool ok = c < W4K && gyy >= 0 && gyy < H && gxx >= 0 && gxx < W;
-        pv[jj] = ok ? (int)((((int64_t)(it.nn * p.cin + c) * H + gyy) * W + gxx) * 4) : SENTINEL;
-    }
-    const int ustep = NXQ * W4K * p.cout * 16;       // bytes of U per K step
-    const int pstep = W4K * (int)plane * 4;           // bytes of input per K step
-    auto issue_u = [&](int ks, int slot) {
-        if constexpr ((PROBE & 1) != 0)
-            if (ks > 0) return;
-        float* us = smem + slot * STAGE;
+        for (int i = 0; i < PPW; ++i) {
+            const int L = (d + 2 * i) * 64 + lane;
+            const int c = L / (ROWS * PCH);
+            const int r2 = L - c * (ROWS * PCH);
+            const int r = r2 / PCH, ch = r2 - r * PCH;
+            const int gyy = 4 * it.ty0 - 1 + r, gxx = 4 * it.tx0 - 4 + 4 * ch;
+            const bool ok = c < W4K && gyy >= 0 && gyy < H && gxx >= 0 && gxx < W;
+            pv[i] = ok ? (int)((((int64_t)(it.nn * p.cin + c) * H + gyy) * W + gxx) * 4) : SENTINEL;
+        }
+        const int ustep = NXQ * W4K * p.cout * 16;
+        const int urun = p.cout * 16;
+        const int pstep = W4K * (int)plane * 4;
+        auto issue_u = [&](int ks, int slot) {
+            if constexpr ((PROBE & 1) != 0)
+                if (ks > 0) return;
+            float* us = smem + slot * STAGE;
 #pragma unroll
-        for (int j = 0; j < UJW; ++j)
-            if (wave + 8 * j < UJ)
+            for (int i = 0; i < UPW; ++i) {
+                const int j = d + 2 * i;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    ursrc, (__attribute__((address_space(3))) void*)(us + (wave + 8 * j) * 256), 16, uv0,
-                    ks * ustep + j * ujs, 0, 0);
-    };
-    auto issue_p = [&](int ks, int slot) {
-        if constexpr ((PROBE & 2) != 0)
-            if (ks > 1) return;
-        float* ps = smem + slot * STAGE + C::UF;
-#pragma unroll
-        for (int jj = 0; jj < PJW; ++jj)
-            if (wave + 8 * jj < PJ) {
-                const int vo = pv[jj];
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    xrsrc, (__attribute__((address_space(3))) void*)(ps + (wave + 8 * jj) * 256), 16, vo, ks * pstep, 0, 0);
+                    ursrc, (__attribute__((address_space(3))) void*)(us + j * 256), 16, uv0, ks * ustep + j * urun, 0, 0);
             }
-    };
+        };
+        auto issue_p = [&](int ks, int slot) {
+            if constexpr ((PROBE & 2) != 0)
+                if (ks > 1) return;
+            float* ps = smem + slot * STAGE + C::UF;
+#pragma unroll
+            for (int i = 0; i < PPW; ++i) {
+                const int jj = d + 2 * i;
+                if (jj < PJ) {
+                    const int vo = pv[i];
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        xrsrc, (__attribute__((address_space(3))) void*)(ps + jj * 256), 16, vo, ks * pstep, 0, 0);
+                }
+            }
+        };
+        issue_u(0, 0);
+        issue_p(0, 0);
+        if (nsteps > 1) issue_p(1, 1);
+        w4_wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        for (int ks = 0; ks < nsteps; ++ks) {
+            __builtin_amdgcn_s_barrier();  // step ks: its U slot and the patch of ks + 1 have landed everywhere
+            asm volatile("" ::: "memory");
+            if (ks + 1 < nsteps) issue_u(ks + 1, (ks + 1) & 1);
+            if (ks + 2 < nsteps) issue_p(ks + 2, ks & 1);
+            w4_wait_vmcnt<0>();
+        }
+        return;
+    }
 
-    // transform role: V of step j is computed by waves [(j & 1) TG, (j & 1) TG + TG), lane -> one (channel, tile)
+    if (wave >= 8) {
+        // ---- transform waves: lane -> patch pi = (wave - 8) 64 + lane = (channel, tile) of the step
+        const int pi = (wave - 8) * 64 + lane;
+        const int tc_ch = pi / TB, tc_t = pi - tc_ch * TB;
+        const int p_off = tc_ch * SLAB + 4 * (tc_t / 16) * PPITCH + 4 * (tc_t % 16) + 3;
+        const int v_off = (tc_ch * NXQ * TB + tc_t) * 4;
+        const float* srow = SM == 1 ? p.s + (int64_t)it.nn * p.cin + tc_ch : nullptr;
+        auto transform = [&](int slot, float sc) {
+            const float* pp = smem + slot * STAGE + C::UF + p_off;
+            float d[6][6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                d[i][0] = pp[i * PPITCH];
+                const f32x4 m = *reinterpret_cast<const f32x4*>(pp + i * PPITCH + 1);
+                d[i][1] = m[0]; d[i][2] = m[1]; d[i][3] = m[2]; d[i][4] = m[3];
+                d[i][5] = pp[i * PPITCH + 5];
+            }
+            float rt[6][6];  // rt[i][b] = (d B)[i][b]
+#pragma unroll
+            for (int i = 0; i < 6; ++i) bt6(d[i], rt[i]);
+            float* vs = smem + slot * STAGE + C::UF + C::PF + v_off;
+            float vv[36];   // xi = 6 b + a
+#pragma unroll
+            for (int b = 0; b < 6; ++b) {
+                float x[6], y[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) x[i] = rt[i][b];
+                bt6(x, y);
+#pragma unroll
+                for (int a = 0; a < 6; ++a) vv[6 * b + a] = SM == 1 ? y[a] * sc : y[a];
+            }
+#pragma unroll
+            for (int q = 0; q < NXQ; ++q)
+                *reinterpret_cast<f32x4*>(vs + q * TB * 4) = f32x4{vv[4 * q], vv[4 * q + 1], vv[4 * q + 2], vv[4 * q + 3]};
+        };
+        // style scale for V(k + 1) loaded during step k - 1
+        float s_nx = SM == 1 && nsteps > 1 ? srow[W4K] : 1.f;
+        const float s0 = SM == 1 ? srow[0] : 1.f;
+        __builtin_amdgcn_s_barrier();
+        transform(0, s0);
+        for (int ks = 0; ks < nsteps; ++ks) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // V(ks) visible; the V slot of ks - 1 is free
+            asm volatile("" ::: "memory");
+            if (ks + 1 < nsteps && ((PROBE & 4) == 0 || ks == 0)) {
+                const float sc = s_nx;
+                if (SM == 1 && ks + 2 < nsteps) s_nx = srow[(ks + 2) * W4K];
+                transform((ks + 1) & 1, sc);
+            }
+        }
+        return;
+    }
+
+    // ---- consumer waves
+    const int cg = wave & 3, tg = wave >> 2;
     const int kq_lane = lane >> 4;
     const int fa_off = (kq_lane * NXQ * OB + 16 * cg + (lane & 15)) * 4;   // A fragment (xq 0) in a U slot
     const int fb_off = (kq_lane * NXQ * TB + 16 * tg + (lane & 15)) * 4;   // B fragment (xq 0) in a V slot
-    const int tw_rel = wave % TG;  // this wave's index among the transform waves of its half
-    const int tpi = tw_rel * 64 + lane;
-    const int tc_ch = tpi / TB, tc_t = tpi - tc_ch * TB;
-    const int p_off = tc_ch * SLAB + 4 * (tc_t / 16) * PPITCH + 4 * (tc_t % 16) + 3;
-    const int v_off = (tc_ch * NXQ * TB + tc_t) * 4;
-    const float* srow = SM == 1 ? p.s + (int64_t)it.nn * p.cin + tc_ch : nullptr;
-    // transform waves of step j: waves 0-3 / 4-7 (TG 4), 0-1 / 2-3 (TG 2) for even / odd j
-    auto tw_step = [&](int j) -> bool {
-        if constexpr (TG == 4) return (wave >> 2) == (j & 1);
-        else return (wave >> 1) == (j & 1);
-    };
-
-    // The transform runs per column pair bp (xi = 6 b + a, b = 2 bp, 2 bp + 1: 12 consecutive values = 3 quads):
-    // the row pass of the pair's two columns over the 6 patch rows (read from LDS again per pair: 12 live values
-    // instead of 36), then the column pass of the two columns, x s[n, c], and 3 ds_write_b128 into the V slot.
-    auto rows_part = [&](int slot, int bp, int i0, float (&rt2)[6][2]) {
-        float xr[3][6];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float* pp = smem + slot * STAGE + C::UF + p_off + (i0 + k) * PPITCH;
-            const f32x4 m = *reinterpret_cast<const f32x4*>(pp + 1);
-            xr[k][1] = m[0]; xr[k][2] = m[1]; xr[k][3] = m[2]; xr[k][4] = m[3];
-            xr[k][0] = bp == 0 ? pp[0] : 0.f;
-            xr[k][5] = bp == 2 ? pp[5] : 0.f;
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float* x = xr[k];
-            float y0, y1;
-            if (bp == 0) {  // (d B)[i][0], [i][1]
-                y0 = __fmaf_rn(4.f, x[0], __fmaf_rn(-5.f, x[2], x[4]));
-                y1 = __fmaf_rn(-4.f, x[1] + x[2], x[3] + x[4]);
-            } else if (bp == 1) {  // [i][2], [i][3]
-                y0 = __fmaf_rn(4.f, x[1] - x[2], x[4] - x[3]);
-                y1 = __fmaf_rn(2.f, x[3] - x[1], x[4] - x[2]);
-            } else {  // [i][4], [i][5]
-                y0 = __fmaf_rn(-2.f, x[3] - x[1], x[4] - x[2]);
-                y1 = __fmaf_rn(4.f, x[1], __fmaf_rn(-5.f, x[3], x[5]));
-            }
-            rt2[i0 + k][0] = y0;
-            rt2[i0 + k][1] = y1;
-        }
-    };
-    auto col_part = [&](int bp, float sc, int slot, const float (&rt2)[6][2]) {
-        float vq[12];
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-            float x[6], y[6];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) x[i] = rt2[i][bb];
-            bt6(x, y);
-#pragma unroll
-            for (int a = 0; a < 6; ++a) vq[6 * bb + a] = SM == 1 ? y[a] * sc : y[a];
-        }
-        float* vs = smem + slot * STAGE + C::UF + C::PF + v_off;
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-            *reinterpret_cast<f32x4*>(vs + (3 * bp + q) * TB * 4) =
-                f32x4{vq[4 * q], vq[4 * q + 1], vq[4 * q + 2], vq[4 * q + 3]};
-    };
-
     f32x4 acc[36];
 #pragma unroll
     for (int xi = 0; xi < 36; ++xi) acc[xi] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // ---- prologue: U(0), P(0), P(1); V(0)
-    issue_u(0, 0);
-    issue_p(0, 0);
-    if (nsteps > 1) issue_p(1, 1);
-    w4_wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    // style scales of the transform: the value for V(k + 1) is loaded during step k - 1 (a global load issued at
-    // the use would stall the transform waves for its round trip every step)
-    float s_nx = SM == 1 && nsteps > 1 ? srow[W4K] : 1.f;
-    if (tw_step(0)) {
-        const float sc = SM == 1 ? srow[0] : 1.f;
-#pragma unroll
-        for (int bp = 0; bp < 3; ++bp) {
-            float rt2[6][2];
-            rows_part(0, bp, 0, rt2);
-            rows_part(0, bp, 3, rt2);
-            col_part(bp, sc, 0, rt2);
-        }
-    }
-
-    // ---- K loop: MFMAs of step k (U slot k & 1, V slot k & 1) with V(k + 1) built by the transform waves
-    // (one body with wave-uniform branches around the transform pieces: two specialised bodies behind one branch
-    // make the compiler merge the accumulators of both at the loop head, which spills them)
-    auto step = [&](int ks, bool tw) {
-        f32x4 fa[2], fb[2];
-        float rt2[6][2];
+    for (int ks = 0; ks < nsteps; ++ks) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of step ks - 1 are done
+        __builtin_amdgcn_s_barrier();  // U(ks), V(ks) in LDS
+        asm volatile("" ::: "memory");
         const int sl = ks & 1;
         const float* us = smem + sl * STAGE + fa_off;
         const float* vs = smem + sl * STAGE + C::UF + C::PF + fb_off;
-        const float sc = s_nx;
-        if (SM == 1 && ks + 2 < nsteps) s_nx = srow[(ks + 2) * W4K];
+        f32x4 fa[2], fb[2];
         fa[0] = *reinterpret_cast<const f32x4*>(us);
         fb[0] = *reinterpret_cast<const f32x4*>(vs);
-        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int xq = 0; xq < NXQ; ++xq) {
             if (xq + 1 < NXQ) {
@@ -308,23 +301,7 @@ void wino4_kernel(Wino4Params p) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 acc[4 * xq + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[xq & 1][j], fb[xq & 1][j], acc[4 * xq + j], 0, 0, 0);
-            if ((PROBE & 4) == 0 && tw) {  // V(k + 1), one third of a column pair per MFMA group
-                if (xq % 3 == 2) col_part(xq / 3, sc, sl ^ 1, rt2);
-                else rows_part(sl ^ 1, xq / 3, 3 * (xq % 3), rt2);
-            }
-            __builtin_amdgcn_sched_barrier(0);
         }
-    };
-    for (int ks = 0; ks < nsteps; ++ks) {
-        if constexpr ((PROBE & 8) == 0) {
-            w4_wait_vmcnt<0>();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();  // U(k), P(k + 1) landed, V(k) written; step k - 1's slots are free
-        }
-        asm volatile("" ::: "memory");
-        if (ks + 1 < nsteps) issue_u(ks + 1, (ks + 1) & 1);
-        if (ks + 2 < nsteps) issue_p(ks + 2, ks & 1);
-        step(ks, ks + 1 < nsteps && tw_step(ks + 1));
     }
 
     // ---- epilogue: Y = A^T M A per (channel, tile), then the conv epilogue
@@ -335,7 +312,7 @@ void wino4_kernel(Wino4Params p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) nz[i][j] = 0.f;
-    float e_d[4], e_b[4];
+    float e_d[4] = {1.f, 1.f, 1.f, 1.f}, e_b[4] = {0.f, 0.f, 0.f, 0.f};
     if (p.mode == SMC_EPI_MODACT) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -437,30 +414,19 @@ __global__ __launch_bounds__(256) void wino4_weights_kernel(const float* w, int 
     }
 }
 
-template <int CG, int TG, int SM, int EK>
-void launch_w4(const Wino4Params& p, int64_t items, hipStream_t st) {
-    hipLaunchKernelGGL((wino4_kernel<CG, TG, SM, EK>), dim3((unsigned)items), dim3(512), 0, st, p);
-}
-
 template <int SM, int EK>
-void launch_w4_cfg(int cg, const Wino4Params& p, int64_t items, hipStream_t st) {
-    if (cg == 4) launch_w4<4, 2, SM, EK>(p, items, st);
-    else launch_w4<2, 4, SM, EK>(p, items, st);
+void launch_w4(const Wino4Params& p, int64_t items, hipStream_t st) {
+    hipLaunchKernelGGL((wino4_kernel<SM, EK>), dim3((unsigned)items), dim3(W4_THREADS), 0, st, p);
 }
 
 template <int EK>
-void launch_w4_s(bool has_s, int cg, const Wino4Params& p, int64_t items, hipStream_t st) {
-    if (has_s) launch_w4_cfg<1, EK>(cg, p, items, st);
-    else launch_w4_cfg<2, EK>(cg, p, items, st);
+void launch_w4_s(bool has_s, const Wino4Params& p, int64_t items, hipStream_t st) {
+    if (has_s) launch_w4<1, EK>(p, items, st);
+    else launch_w4<2, EK>(p, items, st);
 }
 
-// channel groups per work item: 4 (64 output channels x 32 tiles) where cout allows, else 2 (32 x 64)
-int w4_cg(int cout, int h, int w) {
-    if (w % 64 || w < 64) return 0;
-    if (cout % 64 == 0 && h % 8 == 0) return 4;
-    if (cout % 32 == 0 && h % 16 == 0) return 2;
-    return 0;
-}
+// work item = 64 output channels x 32 tiles (2 tile rows x 16 tile columns = 8 x 64 outputs)
+bool w4_shape_ok(int cout, int h, int w) { return w % 64 == 0 && w >= 64 && h % 8 == 0 && cout % 64 == 0; }
 
 }  // namespace
 
@@ -468,7 +434,7 @@ SMC_API int smc_conv3x3_wino4_supported(int n, int cin, int cout, int h, int w) 
     if (n < 1 || cin < W4K || cin % W4K) return 0;
     if ((int64_t)n * cin * h * w * 4 >= (1LL << 31)) return 0;  // raw buffer offsets are 32-bit
     if ((int64_t)cin * 36 * cout * 4 >= (1LL << 31)) return 0;
-    return w4_cg(cout, h, w) != 0;
+    return w4_shape_ok(cout, h, w);
 }
 
 SMC_API int smc_wino4_weights_f32(const float* w, int cout, int cin, int flip, float* uw, void* stream) {
@@ -507,20 +473,18 @@ SMC_API int smc_conv3x3_wino4_f32(const float* x, int n, int cin, int h, int w, 
     p.noise_strength = e.noise_strength; p.bias = e.bias; p.act = e.act; p.alpha = e.alpha; p.gain = e.gain;
     p.clamp = e.clamp; p.u_save = e.u_save;
     p.ext = smc::epi_ext(epi);
-    const int cg = w4_cg(cout, h, w);
-    const int tg = 8 / cg;
     p.gx = w / 64;
-    p.gy = h / (4 * tg);
-    p.ntn = cout / (16 * cg);
+    p.gy = h / 8;
+    p.ntn = cout / 64;
     const int64_t items = (int64_t)n * p.gx * p.gy * p.ntn;
     SMC_CHECK(items < (1LL << 31), "smc_conv3x3_wino4_f32: grid too large");
     hipStream_t st = smc::as_stream(stream);
     const bool modact_plain = p.mode == SMC_EPI_MODACT && !p.ext.residual;
     if (modact_plain && p.act == SMC_ACT_LRELU && p.alpha >= 0.f && p.alpha <= 1.f && p.clamp >= 0.f)
-        launch_w4_s<1>(s_in != nullptr, cg, p, items, st);
+        launch_w4_s<1>(s_in != nullptr, p, items, st);
     else if (modact_plain && p.act == SMC_ACT_LINEAR && p.clamp < 0.f)
-        launch_w4_s<2>(s_in != nullptr, cg, p, items, st);
+        launch_w4_s<2>(s_in != nullptr, p, items, st);
     else
-        launch_w4_s<0>(s_in != nullptr, cg, p, items, st);
+        launch_w4_s<0>(s_in != nullptr, p, items, st);
     return smc::check_launch("smc_conv3x3_wino4_f32");
 }

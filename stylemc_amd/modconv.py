@@ -160,12 +160,23 @@ def wino4_ok(n, cin, cout, h, w):
     return WINOGRAD and bool(_hip.load().smc_conv3x3_wino4_supported(n, cin, cout, h, w))
 
 
+# F(4x4) where it measured faster than F(2x2) (tools/bench_wino.py, FFHQ-1024 batch 4, profiles/r03_wino4/bench_wino_v2.txt):
+# 1.32-1.35x at cin 512 (r = 64), 1.25-1.27x at 256, 1.14-1.16x at 128, 0.99-1.01x at 64 -- the K loop of a
+# 64-channel input (16 steps) is too short to amortise a work item's fill and output transform.  Module switch.
+WINO4 = True
+WINO4_MIN_CIN = 128
+
+
+def wino4_pick(n, cin, cout, h, w):
+    return WINO4 and cin >= WINO4_MIN_CIN and wino4_ok(n, cin, cout, h, w)
+
+
 def wino4(x, y, uw, cin, cout, s=None, epi=None, alg_flops=0.0, alg_bytes=0):
     """One smc_conv3x3_wino4_f32 launch (F(4x4, 3x3)).  alg_flops: the MFMA FLOPs it executes (36 / 144 of the
     direct conv's; the timer also records the direct-equivalent count)."""
     n, _, h, w = x.shape
     tm = _hip.timer()
-    tok = tm.wrap(alg_flops, alg_bytes, kind="wino", equiv_flops=alg_flops * 4) if tm is not None else None
+    tok = tm.wrap(alg_flops, alg_bytes, kind="wino4", equiv_flops=alg_flops * 4) if tm is not None else None
     _hip.call("smc_conv3x3_wino4_f32", x.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(), _hip.ptr(s),
               ctypes.byref(epi) if epi is not None else None, _hip.stream())
     if tok is not None:
@@ -213,10 +224,11 @@ class LayerSpec:
             # runs the original-image synthesis on a side stream): build the Winograd transforms of a Winograd
             # layer now, and let every packing kernel finish before another stream can read the packed weights
             if resolution is not None and up == 1 and P.k == 3:
-                if wino_ok(1, P.cin, P.cout, resolution, resolution):
-                    P.wino_weights(0)
-                if wino_ok(1, P.cout, P.cin, resolution, resolution):
-                    P.wino_weights(1)
+                for flip, (ci, co) in enumerate([(P.cin, P.cout), (P.cout, P.cin)]):
+                    if wino4_pick(1, ci, co, resolution, resolution):
+                        P.wino4_weights(flip)
+                    elif wino_ok(1, ci, co, resolution, resolution):
+                        P.wino_weights(flip)
             torch.cuda.current_stream(weight.device).synchronize()
 
 
@@ -254,7 +266,10 @@ def _modconv_fwd(ctx, x, styles, spec, noise, strength, gain, clamp, need_dx, ne
     epi = _epilogue(_hip.EPI_MODACT, d, nz, nstride, strength, spec.bias, spec.act, spec.alpha, gain, clamp, u)
     phases, nph, th, tw = P.fwd_phases(h, w)
     wbytes = 4 * P.k * P.k * cin * P.cout
-    if spec.up == 1 and P.k == 3 and wino_ok(n, cin, P.cout, h, w):
+    if spec.up == 1 and P.k == 3 and wino4_pick(n, cin, P.cout, h, w):
+        wino4(x, y, P.wino4_weights(0), cin, P.cout, s=styles, epi=epi, alg_flops=wino4_flops(n, cin, P.cout, h, w),
+              alg_bytes=4 * x.numel() + 4 * y.numel() * (2 if u is not None else 1) + 36 * 4 * cin * P.cout)
+    elif spec.up == 1 and P.k == 3 and wino_ok(n, cin, P.cout, h, w):
         wino(x, y, P.wino_weights(0), cin, P.cout, s=styles, epi=epi, alg_flops=wino_flops(n, cin, P.cout, h, w),
              alg_bytes=4 * x.numel() + 4 * y.numel() * (2 if u is not None else 1) + 16 * 4 * cin * P.cout)
     elif spec.up == 1:
@@ -324,7 +339,10 @@ def _modconv_bwd(ctx, saved, gy, need_dx, need_ds, g=None):
         out = dxs
     g_bytes = 4 * g.numel() if spec.up == 1 else 4 * n * P.cout * (2 * h + 1) * (2 * w + 1)
     out_bytes = 4 * out.numel() * (2 if (need_dx and need_ds) else 1)
-    if spec.up == 1 and P.k == 3 and wino_ok(n, P.cout, cin, h, w):
+    if spec.up == 1 and P.k == 3 and wino4_pick(n, P.cout, cin, h, w):
+        wino4(g, out, P.wino4_weights(1), P.cout, cin, epi=ebw, alg_flops=wino4_flops(n, P.cout, cin, h, w),
+              alg_bytes=g_bytes + out_bytes + 36 * 4 * cin * P.cout)
+    elif spec.up == 1 and P.k == 3 and wino_ok(n, P.cout, cin, h, w):
         wino(g, out, P.wino_weights(1), P.cout, cin, epi=ebw, alg_flops=wino_flops(n, P.cout, cin, h, w),
              alg_bytes=g_bytes + out_bytes + 16 * 4 * cin * P.cout)
     else:

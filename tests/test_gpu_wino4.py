@@ -43,15 +43,15 @@ def _check(got, x64, w64, what):
     assert rel <= REL4, f"{what}: relative norm error {rel:.3e}"
 
 
-SHAPES = [  # n, cin, cout, h, w  (CG 4 / CG 2 work items, non-square, 512 channels, cin != cout, cin % 8 == 4)
-    (2, 32, 32, 64, 64),
+SHAPES = [  # n, cin, cout, h, w  (non-square, 512 channels, cin != cout, cin % 8 == 4, several work items per image)
+    (2, 32, 64, 64, 64),
     (1, 64, 64, 64, 64),
-    (2, 16, 32, 128, 128),
-    (1, 32, 64, 256, 128),
+    (2, 16, 64, 128, 128),
+    (1, 64, 128, 256, 128),
     (2, 512, 512, 64, 64),
-    (1, 128, 96, 64, 256),
+    (1, 128, 128, 64, 256),
     (1, 12, 64, 32, 64),
-    (4, 32, 32, 1024, 1024),
+    (4, 64, 64, 512, 512),
 ]
 
 
@@ -72,7 +72,7 @@ def test_wino4_forward_vs_fp64(shape):
            None, H.stream())
     torch.cuda.synchronize()
     assert torch.isfinite(y).all()
-    if n * h * w > 1 << 20:  # the 1024-px case: check the first and last rows of every image (fp64 conv is slow)
+    if n * h * w >= 1 << 20:  # the 512-px case: check the first and last rows of every image (fp64 conv is slow)
         for rows in (slice(0, 64), slice(h - 64, h)):
             xs = x[:, :, max(rows.start - 1, 0):min(rows.stop + 1, h)]
             ref_x = xs.double() * s.double()[:, :, None, None]
@@ -165,8 +165,8 @@ def test_wino4_unsupported_shapes():
     lib = H.load()
     assert lib.smc_conv3x3_wino4_supported(1, 512, 512, 32, 32) == 0   # w < 64
     assert lib.smc_conv3x3_wino4_supported(1, 10, 64, 64, 64) == 0     # cin % 4
-    assert lib.smc_conv3x3_wino4_supported(1, 32, 48, 64, 64) == 0     # cout % 32
-    assert lib.smc_conv3x3_wino4_supported(1, 32, 32, 8, 64) == 0      # cout 32 needs h % 16
+    assert lib.smc_conv3x3_wino4_supported(1, 32, 32, 64, 64) == 0     # cout % 64
+    assert lib.smc_conv3x3_wino4_supported(1, 32, 64, 12, 64) == 0     # h % 8
     x = torch.zeros(1, 32, 32, 32, device=DEV)
     y = torch.zeros(1, 32, 32, 32, device=DEV)
     uw = torch.zeros(36 * 32 * 32, device=DEV)

@@ -1,6 +1,6 @@
 // Where does the F(4x4) Winograd kernel's time go?  Compiles csrc/wino4.hip into this translation unit and times
-// wino4_kernel with pieces removed (PROBE bits: 1 U DMAs after step 0, 2 patch DMAs after step 1, 4 the transform,
-// 8 the per-step wait + barrier) on the synthesis conv1 shapes (batch 4), random data, interleaved repetitions.
+// wino4_kernel with pieces removed (PROBE bits: 1 U DMAs after step 0, 2 patch DMAs after step 1, 4 the transform
+// after step 0) on the synthesis conv1 shapes (batch 4), random data, interleaved repetitions.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -fno-slp-vectorize -I include tools/probes/wino4_probe.hip \
 //         stylemc_amd/csrc/errors.hip -o tools/probes/wino4_probe && tools/probes/wino4_probe
 #include "../../stylemc_amd/csrc/wino4.hip"
@@ -24,31 +24,29 @@ __global__ void fill_kernel(float* p, size_t n, unsigned seed, float scale, floa
     }
 }
 
-template <int CG, int SM, int PROBE>
+template <int SM, int PROBE>
 void launch_p(const Wino4Params& p, int64_t items) {
-    hipLaunchKernelGGL((wino4_kernel<CG, 8 / CG, SM, 0, PROBE>), dim3((unsigned)items), dim3(512), 0, 0, p);
+    hipLaunchKernelGGL((wino4_kernel<SM, 0, PROBE>), dim3((unsigned)items), dim3(W4_THREADS), 0, 0, p);
 }
 
-template <int CG, int SM>
+template <int SM>
 void launch_probe(int probe, const Wino4Params& p, int64_t items) {
     switch (probe) {
-        case 0: launch_p<CG, SM, 0>(p, items); break;
-        case 1: launch_p<CG, SM, 1>(p, items); break;
-        case 2: launch_p<CG, SM, 2>(p, items); break;
-        case 3: launch_p<CG, SM, 3>(p, items); break;
-        case 4: launch_p<CG, SM, 4>(p, items); break;
-        case 7: launch_p<CG, SM, 7>(p, items); break;
-        case 8: launch_p<CG, SM, 8>(p, items); break;
-        case 15: launch_p<CG, SM, 15>(p, items); break;
+        case 0: launch_p<SM, 0>(p, items); break;
+        case 1: launch_p<SM, 1>(p, items); break;
+        case 2: launch_p<SM, 2>(p, items); break;
+        case 3: launch_p<SM, 3>(p, items); break;
+        case 4: launch_p<SM, 4>(p, items); break;
+        case 7: launch_p<SM, 7>(p, items); break;
     }
 }
 
 int main() {
     const int n = 4;
-    const int rs[] = {64, 128, 256, 1024};
-    const int probes[] = {0, 1, 2, 3, 4, 7, 8, 15};
-    const char* names[] = {"full", "-U dma", "-P dma", "-U-P dma", "-transform", "-dma-transform", "-barrier",
-                           "-all"};
+    const int rs[] = {64, 128, 256, 512};
+    const int probes[] = {0, 1, 2, 3, 4, 7};
+    const char* names[] = {"full", "-U dma", "-P dma", "-U-P dma", "-transform", "-dma-transform"};
+    constexpr int NP = 6;
     for (int r : rs) {
         const int c = std::min(32768 / r, 512);
         const size_t nx = (size_t)n * c * r * r;
@@ -64,31 +62,27 @@ int main() {
         Wino4Params p{};
         p.x = x; p.n = n; p.cin = c; p.h = r; p.w = r; p.y = y; p.cout = c; p.uw = uw; p.s = s;
         p.mode = SMC_EPI_STORE; p.act = SMC_ACT_LINEAR; p.gain = 1.f; p.clamp = -1.f;
-        const int cg = w4_cg(c, r, r);
         p.gx = r / 64;
-        p.gy = r / (4 * (8 / cg));
-        p.ntn = c / (16 * cg);
+        p.gy = r / 8;
+        p.ntn = c / 64;
         const int64_t items = (int64_t)n * p.gx * p.gy * p.ntn;
         const double flops = 2.0 * n * c * c * (r / 4) * (r / 4) * 36;
-        float ms[8] = {0};
+        float ms[NP] = {0};
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
         for (int rep = 0; rep < 6; ++rep)
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < NP; ++i) {
                 CK(hipEventRecord(e0));
-                for (int k = 0; k < 5; ++k) {
-                    if (cg == 4) launch_probe<4, 1>(probes[i], p, items);
-                    else launch_probe<2, 1>(probes[i], p, items);
-                }
+                for (int k = 0; k < 5; ++k) launch_probe<1>(probes[i], p, items);
                 CK(hipEventRecord(e1));
                 CK(hipEventSynchronize(e1));
                 float t;
                 CK(hipEventElapsedTime(&t, e0, e1));
                 if (rep > 0) ms[i] += t / 5 / 5;
             }
-        for (int i = 0; i < 8; ++i)
-            std::printf("r=%4d c=%3d cg=%d %-16s %7.1f us  MFMA frac %.3f\n", r, c, cg, names[i], ms[i] * 1e3,
+        for (int i = 0; i < NP; ++i)
+            std::printf("r=%4d c=%3d %-16s %7.1f us  MFMA frac %.3f\n", r, c, names[i], ms[i] * 1e3,
                         flops / (ms[i] * 1e-3) / 157.3e12);
         CK(hipFree(x)); CK(hipFree(y)); CK(hipFree(uw)); CK(hipFree(s));
     }
