@@ -115,13 +115,18 @@ struct W4Item {
 //   waves 8-9   transform: V(k + 1) from the patch of step k + 1 (64 patches each: 18 LDS reads, 2 x 6 six-point
 //               transforms, x s[n, c], 9 ds_write_b128).
 //   waves 10-11 DMA: U(k + 1) and the patch of step k + 2 into their LDS slots (24 LDS-DMAs each), then their wait.
-// Measured before the split (tools/probes/wino4_probe.hip, r = 64): with the transform and the DMAs issued by the MFMA
-// waves, removing the transform took a launch from 338 to 196 us and removing the DMAs to 250 us -- a wave that
-// serialises LDS reads, VALU and DMA issue between its own MFMAs starves the matrix pipe of its SIMD.
+// Measured (tools/probes/wino4_probe.hip, r = 64, profiles/r03_wino4/): with the transform and the DMAs issued by the
+// MFMA waves themselves a launch took 338 us (196 without the transform, 250 without the DMAs) -- a wave that
+// serialises LDS reads, VALU and DMA issue between its own MFMAs starves the matrix pipe of its SIMD; with these
+// roles 232 us (178 without the transform).  Four producer waves (one per SIMD, two lanes per patch with a DPP swap
+// between the row and column pass, a quarter of the DMAs each) measured 243 us: VALU on every SIMD's issue port.
 // SM: style scale s[n, c] (1: present, 2: absent).  EK: epilogue body (1: MODACT lrelu + gain + clamp, 2: MODACT
 // linear, 0: any mode through smc::epi_y / epi_ext_apply).  PROBE (0 in the library; tools/probes/wino4_probe.hip)
 // removes pieces for timing: 1 the U DMAs after step 0, 2 the patch DMAs after step 1, 4 the transform after step 0.
 constexpr int W4_THREADS = 768;
+#ifndef W4_TPRIO
+#define W4_TPRIO 2
+#endif
 
 template <int SM, int EK, int PROBE = 0>
 __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3)))
@@ -129,7 +134,12 @@ void wino4_kernel(Wino4Params p) {
     using C = W4Cfg<4, 2>;
     constexpr int OB = C::OB, TB = C::TB, SLAB = C::SLAB, STAGE = C::STAGE, ROWS = C::ROWS;
     constexpr int UJ = C::UJ, PJ = C::PJ;
-    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+    // + the MODACT epilogue operands of the work item, staged once by the DMA waves: the noise block (8 rows x
+    // 64 columns, x strength) and per output channel d * scale_c and the bias (read by the consumers' epilogue from
+    // LDS, so its loads neither stall behind its own stores nor hold registers across the output transform)
+    constexpr int EPI_F = 8 * 64 + 2 * 64;
+    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + EPI_F];
+    float* epi_s = smem + 2 * STAGE;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -208,7 +218,27 @@ void wino4_kernel(Wino4Params p) {
         issue_u(0, 0);
         issue_p(0, 0);
         if (nsteps > 1) issue_p(1, 1);
+        if (p.mode == SMC_EPI_MODACT) {
+            const int pt = d * 64 + lane;  // 128 lanes: noise floats 4 pt .. 4 pt + 3; channel pt < 64
+            const int yy = 4 * it.ty0 + (4 * pt) / 64, xx = 4 * it.tx0 + (4 * pt) % 64;
+            const float nstr = p.noise ? (p.noise_strength ? *p.noise_strength : 1.f) : 0.f;
+            const f32x4 nz = p.noise ? *reinterpret_cast<const f32x4*>(p.noise + it.nn * p.noise_nstride +
+                                                                        (int64_t)yy * W + xx)
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+            float dv = 0.f, bv = 0.f;
+            if (pt < 64) {
+                const int o = it.o0 + pt;
+                dv = (p.d ? p.d[(int64_t)it.nn * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
+                bv = p.bias ? p.bias[o] : 0.f;
+            }
+            *reinterpret_cast<f32x4*>(epi_s + 4 * pt) = nz * nstr;
+            if (pt < 64) {
+                epi_s[512 + pt] = dv;
+                epi_s[576 + pt] = bv;
+            }
+        }
         w4_wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         for (int ks = 0; ks < nsteps; ++ks) {
             __builtin_amdgcn_s_barrier();  // step ks: its U slot and the patch of ks + 1 have landed everywhere
@@ -227,6 +257,9 @@ void wino4_kernel(Wino4Params p) {
         const int p_off = tc_ch * SLAB + 4 * (tc_t / 16) * PPITCH + 4 * (tc_t % 16) + 3;
         const int v_off = (tc_ch * NXQ * TB + tc_t) * 4;
         const float* srow = SM == 1 ? p.s + (int64_t)it.nn * p.cin + tc_ch : nullptr;
+        // the transform is the step's long pole: its VALU goes ahead of the consumers' (their MFMAs queue on the
+        // matrix pipe anyway) -- issue arbitration is by priority, then age, and these waves are the youngest
+        __builtin_amdgcn_s_setprio(W4_TPRIO);
         auto transform = [&](int slot, float sc) {
             const float* pp = smem + slot * STAGE + C::UF + p_off;
             float d[6][6];
@@ -307,29 +340,7 @@ void wino4_kernel(Wino4Params p) {
     // ---- epilogue: Y = A^T M A per (channel, tile), then the conv epilogue
     const int nn = it.nn;
     const int yy0 = 4 * (it.ty0 + tg), xx0 = 4 * (it.tx0 + (lane & 15));
-    float nz[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) nz[i][j] = 0.f;
-    float e_d[4] = {1.f, 1.f, 1.f, 1.f}, e_b[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.mode == SMC_EPI_MODACT) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int o = it.o0 + 16 * cg + 4 * kq_lane + r;
-            e_d[r] = (p.d ? p.d[(int64_t)nn * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
-            e_b[r] = p.bias ? p.bias[o] : 0.f;
-        }
-        if (p.noise) {
-            const float nstr = p.noise_strength ? *p.noise_strength : 1.f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const f32x4 q = *reinterpret_cast<const f32x4*>(p.noise + nn * p.noise_nstride + (int64_t)(yy0 + i) * W + xx0);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) nz[i][j] = q[j] * nstr;
-            }
-        }
-    }
+    const bool modact = p.mode == SMC_EPI_MODACT;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int o = it.o0 + 16 * cg + 4 * kq_lane + r;
@@ -350,18 +361,21 @@ void wino4_kernel(Wino4Params p) {
             at6(zc[i], out);
             const int64_t idx = obase + (int64_t)(yy0 + i) * W + xx0;
             float q[4];
-            if (EK != 0 || p.mode == SMC_EPI_MODACT) {
+            if (EK != 0 || modact) {
                 if (p.u_save) *reinterpret_cast<f32x4*>(p.u_save + idx) = f32x4{out[0], out[1], out[2], out[3]};
-                const float dsc = e_d[r], bo = e_b[r];
+                const int ol = 16 * cg + 4 * kq_lane + r;
+                const float dsc = epi_s[512 + ol], bo = epi_s[576 + ol];
+                const f32x4 nq = *reinterpret_cast<const f32x4*>(epi_s + (4 * tg + i) * 64 + 4 * (lane & 15));
+                const float nz[4] = {nq[0], nq[1], nq[2], nq[3]};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if constexpr (EK == 1) {
-                        const float z = __fmaf_rn(out[j], dsc, nz[i][j]) + bo;
+                        const float z = __fmaf_rn(out[j], dsc, nz[j]) + bo;
                         q[j] = fmaxf(fminf(fmaxf(z, z * p.alpha) * p.gain, p.clamp), -p.clamp);
                     } else if constexpr (EK == 2) {
-                        q[j] = (__fmaf_rn(out[j], dsc, nz[i][j]) + bo) * p.gain;
+                        q[j] = (__fmaf_rn(out[j], dsc, nz[j]) + bo) * p.gain;
                     } else {
-                        q[j] = smc::epi_y(out[j], dsc, nz[i][j], bo, p.act, p.alpha, p.gain, p.clamp);
+                        q[j] = smc::epi_y(out[j], dsc, nz[j], bo, p.act, p.alpha, p.gain, p.clamp);
                         if (p.ext.residual)
                             q[j] = smc::epi_ext_apply(SMC_EPI_STORE, q[j], nn, o, idx + j, yy0 + i, xx0 + j, p.cout, H,
                                                       W, nullptr, nullptr, p.ext);

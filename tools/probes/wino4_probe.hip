@@ -43,7 +43,7 @@ void launch_probe(int probe, const Wino4Params& p, int64_t items) {
 
 int main() {
     const int n = 4;
-    const int rs[] = {64, 128, 256, 512};
+    const int rs[] = {64, 128, 256};
     const int probes[] = {0, 1, 2, 3, 4, 7};
     const char* names[] = {"full", "-U dma", "-P dma", "-U-P dma", "-transform", "-dma-transform"};
     constexpr int NP = 6;

@@ -68,10 +68,18 @@ def main():
 
     variants = {"default": (clip, idl, {}), "no_clip": ([(free, 1.0)], idl, {}), "no_irse": (clip, free, {}),
                 "no_losses": ([(free, 1.0)], free, {}), "no_prefetch": (clip, idl, dict(prefetch_orig=False)),
-                "irse_pair": (clip, idl, dict(prefetch_id=False))}
+                "irse_pair": (clip, idl, dict(prefetch_id=False)), "side_hi": (clip, idl, {}),
+                "main_side_hi": (clip, idl, {})}
     name = sys.argv[sys.argv.index("--variant") + 1]
     clips, idloss, kw = variants[name]
-    ms = timed(finder(clips, idloss, **kw), steps)
+    f = finder(clips, idloss, **kw)
+    # stream priority variants: the IR-SE50 (side) stream -- or it and the main stream (edited synthesis, CLIP,
+    # backward) -- at high priority; the prefetch stream (next iteration's original image) stays normal
+    if name in ("side_hi", "main_side_hi"):
+        f._side = torch.cuda.Stream(device=dev, priority=-1)
+    main = torch.cuda.Stream(device=dev, priority=-1) if name == "main_side_hi" else torch.cuda.current_stream()
+    with torch.cuda.stream(main):
+        ms = timed(f, steps)
     print(f"{name:12s} {ms:7.2f} ms/step", flush=True)
 
 
