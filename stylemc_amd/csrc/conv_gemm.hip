@@ -1640,12 +1640,10 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         else if (cfg == 0 && lds_bk32(cfg, cin))
             hipLaunchKernelGGL((conv_gemm_lds_kernel<2, 2, 2, 2, 32, 2>), grid, dim3(NT), 0, st, p);
         else if (cfg == 0) SMC_LAUNCH_LDS(2, 2, 2, 2);
-#ifdef SMC_AB_SMALL_BK32
+        // IR-SE50 (TAG 1) 64x64 tiles: 32-channel K steps (half the barriers of a 9-step split):
+        // f(4) + b(4) 3.57 -> 3.52 ms (profiles/r03_irse_bk32_ab.txt)
         else if (cfg == 3 && cin % 32 == 0 && tag)
             hipLaunchKernelGGL((conv_gemm_lds_kernel<2, 2, 1, 1, 32, 2, 1>), grid, dim3(NT), 0, st, p);
-        else if (cfg == 3 && cin % 32 == 0)
-            hipLaunchKernelGGL((conv_gemm_lds_kernel<2, 2, 1, 1, 32, 2>), grid, dim3(NT), 0, st, p);
-#endif
         else if (cfg == 3) SMC_LAUNCH_LDS(2, 2, 1, 1);
         else if (cfg == 4) SMC_LAUNCH_LDS(1, 4, 1, 1);
         else SMC_LAUNCH_LDS(2, 2, 1, 2);

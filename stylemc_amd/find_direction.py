@@ -133,7 +133,7 @@ class DirectionFinder:
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
                  overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None, G2=None, temp_shapes2=None,
-                 prefetch_id=True):
+                 prefetch_id=True, prefetch_clip=False):
         self.G = G
         # the edited image's generator (train_latent_mapper.py:100-106,159-162 --network2; default G itself)
         self.G_edit = G2 if G2 is not None else G
@@ -149,6 +149,8 @@ class DirectionFinder:
         # (tools/sensitivity.py: dropping it saves 1.8 ms, dropping CLIP nothing), so its critical-path share is
         # cut to the edited images' forward + backward; CLIP keeps the [edited; original] batch
         self.prefetch_id = prefetch_id
+        # ... and its CLIP embeddings (then CLIP too sees only the edited images on the critical path)
+        self.prefetch_clip = prefetch_clip
         self._next_i = None
         self._pref = None
         # edited + original image through each loss network as ONE batch (backward for the edited half)
@@ -236,16 +238,17 @@ class DirectionFinder:
         rows); then each loss network sees [edited; original] as one batch."""
         side = self._side_stream()
         pref, self._pref = self._pref, None
-        y_feats = None
+        y_feats = src_embs = None
         if side is not None and pref is not None and pref[0] == key:
             main = torch.cuda.current_stream()
             img = self._synth_edited(styles, d)
             main.wait_stream(self._pre)
             orig = pref[1]
             orig.record_stream(main)
-            y_feats = pref[2]
-            if y_feats is not None:
-                y_feats.record_stream(main)
+            y_feats, src_embs = pref[2], pref[3]
+            for t in [y_feats] + (src_embs or []):
+                if t is not None:
+                    t.record_stream(main)
         elif side is not None:
             main = torch.cuda.current_stream()
             side.wait_stream(main)
@@ -272,8 +275,12 @@ class DirectionFinder:
                             else self.id_loss.per_sample_pair(img, orig))
         else:
             id_terms = self.id_loss.per_sample_pair(img, orig)
-        clip_terms = sum(w * cl.per_sample_pair(t, s) for (cl, w), (t, s) in zip(self.clip_losses,
-                                                                                  self._clip_inputs(img, orig)))
+        if src_embs is not None:
+            clip_terms = sum(w * cl.per_sample_with(e, t) for (cl, w), (t, _), e in
+                             zip(self.clip_losses, self._clip_inputs(img, None), src_embs))
+        else:
+            clip_terms = sum(w * cl.per_sample_pair(t, s) for (cl, w), (t, s) in zip(self.clip_losses,
+                                                                                      self._clip_inputs(img, orig)))
         if side is not None:
             main.wait_stream(side)
             id_terms.record_stream(main)
@@ -343,7 +350,9 @@ class DirectionFinder:
         with torch.cuda.stream(self._pre), torch.no_grad():
             orig = self.synth_fn(self.G, self.until_k, self.styles_array[a:b], self.temp_shapes, self.noise_mode)
             feats = self.id_loss.target_feats(orig) if self.prefetch_id else None
-        self._pref = ((a, b), orig, feats)
+            embs = ([cl.encode_src(s) for (cl, _), (_, s) in zip(self.clip_losses, self._clip_inputs(None, orig))]
+                    if self.prefetch_clip else None)
+        self._pref = ((a, b), orig, feats, embs)
 
     def step(self):
         self.it += 1
