@@ -90,6 +90,8 @@ typedef struct {
     int out_oy, out_ox;   /* offset of the grid in y                          */
     int out_sy, out_sx;   /* stride of the grid in y                          */
     const float* wk;      /* [ntaps][cin][cout] packed weights                */
+    const float* wino_u;  /* optional (IR-SE50 executor): Winograd F(2x2) taps of a 9-tap 3x3 stride-1 'same'
+                             phase from smc_wino_taps_f32, used for its <= 16x16 planes; NULL = none        */
 } smc_conv_phase;
 
 #define SMC_EPI_STORE 0   /* y = acc                                                           */
@@ -154,6 +156,16 @@ int smc_conv3x3_wino4_f32(const float* x, int n, int cin, int h, int w, float* y
 /* w [cout][cin][3][3] -> uw [K][9][N][4] floats (36 * cin * cout, 16-B aligned), U = G g G^T (6x6) per (k, n) computed
  * in fp64 and rounded once, element (a, b) at xi = 6 b + a; flip as for smc_wino_weights_f32. */
 int smc_wino4_weights_f32(const float* w, int cout, int cin, int flip, float* uw, void* stream);
+
+/* Small-plane Winograd F(2x2, 3x3) with split-K for the IR-SE50 14x14 / 7x7 stages (id_loss/model_irse.py,
+ * helpers.py:86-119): the 3x3 stride-1 'same' conv of a 9-tap phase, x [n][cin][h][w] -> y [n][cout][h][w], any
+ * smc_conv_epilogue mode applied by the split-K reduction (smc_modconv_epilogue_f32).  uw from smc_wino_taps_f32
+ * ([cin][4][cout][4]).  Supported: h, w in [2, 16], cin % 8 == 0 (>= 16), cout % 32 == 0. */
+int smc_wino_sp_supported(int n, int cin, int cout, int h, int w);
+int64_t smc_wino_sp_workspace_size(int n, int cin, int cout, int h, int w);
+int smc_wino_taps_f32(const smc_conv_phase* phase, int cin, int cout, float* uw, void* stream);
+int smc_conv3x3_wino_sp_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
+                            const smc_conv_epilogue* epi, float* workspace, int64_t workspace_bytes, void* stream);
 
 /* Apply the modconv epilogue to a raw accumulator tensor, summing `nsplit` partial planes
  * (src + k*split_stride).  src/y/u_save: [n, c, h, w]. */

@@ -23,7 +23,7 @@ EPI_STORE, EPI_MODACT, EPI_PRELU, EPI_PRELU_GRAD, EPI_AFFINE = 0, 1, 2, 3, 4
 class ConvPhase(ctypes.Structure):
     _fields_ = [("ntaps", c_int), ("tap_dy", c_int * 9), ("tap_dx", c_int * 9), ("in_stride", c_int),
                 ("out_h", c_int), ("out_w", c_int), ("out_oy", c_int), ("out_ox", c_int), ("out_sy", c_int),
-                ("out_sx", c_int), ("wk", c_void_p)]
+                ("out_sx", c_int), ("wk", c_void_p), ("wino_u", c_void_p)]
 
 
 class ConvEpilogue(ctypes.Structure):
@@ -62,6 +62,10 @@ _SIGS = {
     "smc_conv3x3_wino4_supported": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "smc_conv3x3_wino4_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P]),
     "smc_wino4_weights_f32": (c_int, [P, c_int, c_int, c_int, P, P]),
+    "smc_wino_sp_supported": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "smc_wino_sp_workspace_size": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
+    "smc_wino_taps_f32": (c_int, [P, c_int, c_int, P, P]),
+    "smc_conv3x3_wino_sp_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_int64, P]),
     "smc_modconv_epilogue_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, P, P]),
     "smc_modconv_blur_act_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                          c_int, c_int, c_int, c_int, c_float, c_int, P, P]),

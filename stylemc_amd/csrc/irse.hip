@@ -278,6 +278,7 @@ int64_t conv_ws_need(const smc_irse_net& net, int n) {
     int64_t m = 0;
     auto q = [&](int cin, int cout, int yh, int yw, const smc_conv_phase* ph, int nph) {
         m = std::max(m, smc::conv_gemm_aux_workspace_size(n, cin, cout, yh, yw, ph, nph));
+        if (nph == 1 && ph->wino_u) m = std::max(m, smc_wino_sp_workspace_size(n, cin, cout, yh, yw));
     };
     q(net.stem_cin, net.stem_cout, net.in_h, net.in_w, &net.stem_fwd, 1);
     q(net.stem_cout, net.stem_cin, net.in_h, net.in_w, &net.stem_bwd, 1);
@@ -386,6 +387,8 @@ SMC_API int smc_irse_forward_f32(const smc_irse_net* net, const float* img, int 
     if (saved) saved_floats(*net, n, saved, us.data(), &stem_z);
     auto conv = [&](const float* x, int cin, int ih, int iw, float* y, int cout, int yh, int yw,
                     const smc_conv_phase* ph, int nph, const smc_conv_epilogue& e) {
+        if (nph == 1 && ph->wino_u && ih == yh && iw == yw && smc_wino_sp_supported(n, cin, cout, ih, iw))
+            return smc_conv3x3_wino_sp_f32(x, n, cin, ih, iw, y, cout, ph->wino_u, &e, w.conv, w.conv_bytes, stream);
         return smc::conv_gemm_aux(x, n, cin, ih, iw, y, cout, yh, yw, ph, nph, nullptr, &e, w.conv, w.conv_bytes,
                                  stream);
     };
@@ -471,6 +474,8 @@ SMC_API int smc_irse_backward_f32(const smc_irse_net* net, const float* dfeat, i
     saved_floats(*net, n_saved, const_cast<float*>(saved), us.data(), &stem_z);
     auto conv = [&](const float* x, int cin, int ih, int iw, float* y, int cout, int yh, int yw,
                     const smc_conv_phase* ph, int nph, const smc_conv_epilogue& e) {
+        if (nph == 1 && ph->wino_u && ih == yh && iw == yw && smc_wino_sp_supported(n, cin, cout, ih, iw))
+            return smc_conv3x3_wino_sp_f32(x, n, cin, ih, iw, y, cout, ph->wino_u, &e, w.conv, w.conv_bytes, stream);
         return smc::conv_gemm_aux(x, n, cin, ih, iw, y, cout, yh, yw, ph, nph, nullptr, &e, w.conv, w.conv_bytes,
                                  stream);
     };

@@ -19,6 +19,9 @@ from .id_loss.model_irse import Backbone
 from .modconv import _phase
 
 P = ctypes.c_void_p
+# The 3x3 stride-1 convs of the <= 16x16 stages (14x14 x 256, 7x7 x 512) and their adjoints run as small-plane
+# Winograd F(2x2, 3x3) with split-K (csrc/wino_sp.hip); module switch (tests / tools flip it for the direct GEMM).
+WINO_SP = True
 
 
 class IrseUnit(ctypes.Structure):
@@ -93,6 +96,19 @@ class _Packed:
                     wks.append(adj_weight(W, ky, kx, in_scale, out_scale))
             return phase(taps, 1, h, w, torch.stack(wks))
 
+        lib = _hip.load()
+
+        def wino(ph, cin, cout, hw):
+            """Small-plane Winograd taps (smc_wino_taps_f32) for a 9-tap 3x3 stride-1 'same' phase whose planes
+            (hw x hw) the smc_conv3x3_wino_sp_f32 kernel takes: the executor then runs that conv as F(2x2, 3x3)."""
+            if not WINO_SP or not lib.smc_wino_sp_supported(1, cin, cout, hw, hw):
+                return ph
+            uw = torch.empty(16 * cin * cout, device=dev, dtype=torch.float32)
+            _hip.call("smc_wino_taps_f32", ctypes.byref(ph), cin, cout, uw.data_ptr(), _hip.stream())
+            self.keep.append(uw)
+            ph.wino_u = uw.data_ptr()
+            return ph
+
         def stride2_adjoint(W, oh, ow, out_scale):
             # forward out[a] = sum_k W[k] x[2a + k - 1]  ->  d x[2a+p] gathers (p=0: k=1 at a; p=1: k=2 at a, k=0 at a+1)
             sel = {0: [(0, 1)], 1: [(0, 2), (1, 0)]}
@@ -141,13 +157,14 @@ class _Packed:
             a2, b2 = bn_affine(bn2)
             u.bn1_a, u.bn1_b = ptr(a1), ptr(b1)
             taps, wk = fwd_taps(W1)
-            u.c1_fwd = phase(taps, 1, hw, hw, wk)
-            u.c1_bwd = same_adjoint(W1, hw, hw, in_scale=a1)
+            u.c1_fwd = wino(phase(taps, 1, hw, hw, wk), u.cin, u.depth, hw)
+            u.c1_bwd = wino(same_adjoint(W1, hw, hw, in_scale=a1), u.depth, u.cin, hw)
             u.prelu = ptr(pr.weight)
             taps, wk = fwd_taps(W2)
             u.c2_fwd = phase(taps, s, oh, oh, wk)
             if s == 1:
-                u.c2_bwd[0] = same_adjoint(W2, hw, hw, out_scale=a2)
+                u.c2_fwd = wino(u.c2_fwd, u.depth, u.depth, hw)
+                u.c2_bwd[0] = wino(same_adjoint(W2, hw, hw, out_scale=a2), u.depth, u.depth, hw)
                 u.c2_bwd_nphases = 1
             else:
                 for i, ph in enumerate(stride2_adjoint(W2, oh, oh, a2)):
@@ -186,6 +203,8 @@ class _Packed:
         fb = fb * af + bf
         nt.feat, nt.flat = feat, flat
         nt.fc_wt, nt.fc_w, nt.fc_b = ptr(Wf.t()), ptr(Wf), ptr(fb)
+        if dev.type == "cuda":  # the packed weights (and Winograd taps) are complete before any stream reads them
+            torch.cuda.current_stream(dev).synchronize()
 
 
 class _IrseFn(torch.autograd.Function):
