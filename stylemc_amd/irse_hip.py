@@ -101,8 +101,8 @@ class _Packed:
         def wino(ph, cin, cout, hw):
             """Small-plane Winograd taps (smc_wino_taps_f32) for a 9-tap 3x3 stride-1 'same' phase whose planes
             (hw x hw) the smc_conv3x3_wino_sp_f32 kernel takes: the executor then runs that conv as F(2x2, 3x3)."""
-            if not WINO_SP or not lib.smc_wino_sp_supported(1, cin, cout, hw, hw):
-                return ph
+            if not WINO_SP or dev.type != "cuda" or not lib.smc_wino_sp_supported(1, cin, cout, hw, hw):
+                return ph  # (a host-side descriptor build keeps the implicit-GEMM phases; the taps are device data)
             uw = torch.empty(16 * cin * cout, device=dev, dtype=torch.float32)
             _hip.call("smc_wino_taps_f32", ctypes.byref(ph), cin, cout, uw.data_ptr(), _hip.stream())
             self.keep.append(uw)
