@@ -140,6 +140,13 @@ int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w, float*
 int smc_conv3x3_wino_supported(int n, int cin, int cout, int h, int w);
 int smc_conv3x3_wino_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
                          const float* s_in, const smc_conv_epilogue* epi, void* stream);
+/* The same conv with split K for grids too small to fill the chip (smc_conv3x3_wino_workspace_size() > 0: fewer than
+ * 512 work items): K splits write raw partial tiles into `workspace` and smc_modconv_epilogue_f32 sums them and
+ * applies `epi`.  A NULL / too small workspace runs the single-pass kernel. */
+int64_t smc_conv3x3_wino_workspace_size(int n, int cin, int cout, int h, int w);
+int smc_conv3x3_wino_ws_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
+                            const float* s_in, const smc_conv_epilogue* epi, float* workspace, int64_t workspace_bytes,
+                            void* stream);
 /* w [cout][cin][3][3] -> uw [K][4][N][4] floats (16 * cin * cout, 16-B aligned), U = G g G^T per (k, n):
  * flip = 0: K = cin, N = cout, g = w[n][k] (the forward correlation);
  * flip = 1: K = cout, N = cin, g = w[k][n] rotated 180 degrees (the data gradient, conv^T). */

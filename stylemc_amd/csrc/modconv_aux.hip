@@ -176,6 +176,8 @@ inline dim3 fir_grid_fwd(int64_t planes, int w, int h) {
     return dim3((unsigned)smc::ceil_div(w, kFW), (unsigned)smc::ceil_div(h, kFH), (unsigned)planes);
 }
 
+// (explicit fmaf: every kernel that shares these helpers rounds the same way whatever the compiler's contraction and
+// packed-math choices in its context -- the 16-B, strip and scalar-load kernels agree bit for bit)
 template <int FH, int FW>
 __device__ __forceinline__ void fir_block(const float* tile, int stride, int ly0, int lx0, const float (&tp)[FH][FW],
                                           float (&out)[4][2]) {
@@ -193,7 +195,7 @@ __device__ __forceinline__ void fir_block(const float* tile, int stride, int ly0
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int jx = 0; jx < FW; ++jx) out[i][j] += tp[jy][jx] * v[j + jx];
+                for (int jx = 0; jx < FW; ++jx) out[i][j] = __fmaf_rn(tp[jy][jx], v[j + jx], out[i][j]);
         }
     }
 }
@@ -219,7 +221,7 @@ __device__ __forceinline__ void fir_block_split(const float* tile, int stride, i
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int jx = 0; jx < FW; ++jx) out[i][j] += tp[jy][jx] * v[j][jx];
+                for (int jx = 0; jx < FW; ++jx) out[i][j] = __fmaf_rn(tp[jy][jx], v[j][jx], out[i][j]);
         }
     }
 }

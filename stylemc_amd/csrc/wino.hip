@@ -56,6 +56,9 @@ struct WinoParams {
     smc::EpiExt ext;
     int gx, gy;  // tile groups per image along x / y
     int ntn;     // output-channel blocks (cout / 32)
+    int nsplit;            // K splits (grid.y): > 1 stores raw partial tiles (EK 3) for smc_modconv_epilogue_f32
+    int64_t split_stride;  // floats between the partial planes of two splits
+    float* ws;             // the partial planes [nsplit][n][cout][h][w]
 };
 
 template <int TC>
@@ -93,7 +96,8 @@ struct WinoItem {
 // workgroups as fit on the chip and each loops over work items (stride gridDim.x); the next item's first DMA is
 // issued during the current item's last K step, so the K loop's fill latency and the epilogue of one item overlap
 // instead of starting every workgroup cold -- what the 4-step (cin 32) and 8-step (cin 64) layers lost most to.
-// EK: the epilogue body, chosen at launch (1: MODACT lrelu + gain + clamp, 2: MODACT linear, 0: any mode).
+// EK: the epilogue body, chosen at launch (1: MODACT lrelu + gain + clamp, 2: MODACT linear, 0: any mode, 3: the raw
+// output tiles of a K split into the workspace -- the split-K form, p.nsplit > 1, grid.y = split).
 template <int TC, int SM, int EK, int PERSIST, int PROBE = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void wino_kernel(WinoParams p) {
@@ -107,7 +111,8 @@ void wino_kernel(WinoParams p) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int H = p.h, W = p.w;
     const int64_t plane = (int64_t)H * W;
-    const int nsteps = p.cin / WBK;
+    const int nsteps = p.cin / WBK / p.nsplit;  // this workgroup's K steps: channels [kb WBK, (kb + nsteps) WBK)
+    const int kb = (int)blockIdx.y * nsteps;
     const int total = p.n * p.gx * p.gy * p.ntn;
     const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * plane * 4), 0x00020000);
@@ -153,7 +158,7 @@ void wino_kernel(WinoParams p) {
     // (2 TR + 2) x (2 TC + 8) patch (16-B chunks from column 2 tx0 - 4, zero-filled by the buffer range check)
     auto issue = [&](const int (&uv)[UJW], const int (&pv)[PJW], int ks, int slot) {
         float* us = smem + slot * STAGE;
-        const int uso = ks * (WBK * 16 * 4) * p.cout;
+        const int uso = (kb + ks) * (WBK * 16 * 4) * p.cout;
 #pragma unroll
         for (int j = 0; j < ((PROBE & 1) != 0 && ks > 0 ? 0 : UJW); ++j) {
             const int vo = uv[j];  // (through a local: hipcc drops the kernel's host stub when the array is passed)
@@ -163,7 +168,7 @@ void wino_kernel(WinoParams p) {
         if constexpr ((PROBE & 2) != 0)
             if (ks > 0) return;
         float* ps = us + C::UF;
-        const int pso = ks * WBK * (int)plane * 4;
+        const int pso = (kb + ks) * WBK * (int)plane * 4;
 #pragma unroll
         for (int jj = 0; jj < PJW; ++jj)
             if (wave + NW * jj < C::PJ) {
@@ -188,7 +193,7 @@ void wino_kernel(WinoParams p) {
     int uv[UJW], pv[PJW];
     offsets(it, uv, pv);
     issue(uv, pv, 0, 0);
-    const float* srow = has_s ? p.s + (int64_t)it.nn * p.cin + kq_lane : p.x;
+    const float* srow = has_s ? p.s + (int64_t)it.nn * p.cin + kb * WBK + kq_lane : p.x;
     float sv[2] = {1.f, 1.f}, sn[2] = {1.f, 1.f};
     if (has_s) { sn[0] = srow[0]; sn[1] = srow[4]; }
     int gs = 0;  // K steps run by this workgroup so far: LDS slot gs & 1
@@ -329,7 +334,7 @@ void wino_kernel(WinoParams p) {
             // The MODACT epilogue's per-channel / per-pixel operands, all loaded before the first store (issued after
             // a store that may alias them, each would wait out that store's round trip)
             float e_d[OBW][4], e_b[OBW][4], nz[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-            if (p.mode == SMC_EPI_MODACT) {
+            if (EK != 3 && p.mode == SMC_EPI_MODACT) {
 #pragma unroll
                 for (int b = 0; b < OBW; ++b)
 #pragma unroll
@@ -375,7 +380,13 @@ void wino_kernel(WinoParams p) {
                             out[i][1] = rr[i][1] - rr[i][2] - rr[i][3];
                         }
                         const int64_t obase = ((int64_t)nn * p.cout + o) * plane;
-                        if (KIND != 0 || p.mode == SMC_EPI_MODACT) {
+                        if constexpr (KIND == 3) {
+                            float* wp = p.ws + blockIdx.y * p.split_stride;
+#pragma unroll
+                            for (int i = 0; i < 2; ++i)
+                                *reinterpret_cast<float2*>(wp + obase + (int64_t)(yy0 + i) * W + xx0) =
+                                    make_float2(out[i][0], out[i][1]);
+                        } else if (KIND != 0 || p.mode == SMC_EPI_MODACT) {
                             const float dsc = e_d[b][r], bo = e_b[b][r];
 #pragma unroll
                             for (int i = 0; i < 2; ++i) {
@@ -471,7 +482,7 @@ int wino_tc(int h, int w) {
 // tools/probes/wino_ab.hip, profiles/r03_wino_ab.txt.)
 template <int TC, int SM, int EK>
 void launch_wino(const WinoParams& p, int64_t items, hipStream_t st) {
-    hipLaunchKernelGGL((wino_kernel<TC, SM, EK, 0>), dim3((unsigned)items), dim3(256), 0, st, p);
+    hipLaunchKernelGGL((wino_kernel<TC, SM, EK, 0>), dim3((unsigned)items, (unsigned)p.nsplit), dim3(256), 0, st, p);
 }
 
 template <int SM, int EK>
@@ -485,6 +496,25 @@ template <int EK>
 void launch_wino_s(bool has_s, int tc, const WinoParams& p, int64_t items, hipStream_t st) {
     if (has_s) launch_wino_tc<1, EK>(tc, p, items, st);
     else launch_wino_tc<2, EK>(tc, p, items, st);
+}
+
+// K splits of a launch: a grid of fewer than two workgroups per CU (the kernel's occupancy) leaves each SIMD one
+// wave to hide the DMA and LDS latency with -- the 32 x 32 synthesis conv of cin 512 (256 items, 64 K steps) ran at
+// a quarter of the MFMA rate.  Split K (a power of two dividing the step count, >= 8 steps per split) until the grid
+// holds kWinoSplitTarget workgroups; the partial tiles are summed by the modconv epilogue kernel.
+#ifndef SMC_WINO_SPLIT_TARGET
+#define SMC_WINO_SPLIT_TARGET 512
+#endif
+constexpr int64_t kWinoSplitTarget = SMC_WINO_SPLIT_TARGET;
+
+int wino_nsplit(int n, int cin, int cout, int h, int w) {
+    const int tc = wino_tc(h, w);
+    if (!tc) return 1;
+    const int64_t items = (int64_t)n * ((w / 2) / tc) * ((h / 2) / (WBT / tc)) * (cout / WBO);
+    const int nsteps = cin / WBK;
+    int ns = 1;
+    while (items * ns < kWinoSplitTarget && nsteps % (2 * ns) == 0 && nsteps / (2 * ns) >= 8) ns *= 2;
+    return ns;
 }
 
 }  // namespace
@@ -504,8 +534,20 @@ SMC_API int smc_wino_weights_f32(const float* w, int cout, int cin, int flip, fl
     return smc::check_launch("smc_wino_weights_f32");
 }
 
+SMC_API int64_t smc_conv3x3_wino_workspace_size(int n, int cin, int cout, int h, int w) {
+    if (!smc_conv3x3_wino_supported(n, cin, cout, h, w)) return 0;
+    const int ns = wino_nsplit(n, cin, cout, h, w);
+    return ns > 1 ? (int64_t)ns * n * cout * h * w * 4 : 0;
+}
+
 SMC_API int smc_conv3x3_wino_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
                                  const float* s_in, const smc_conv_epilogue* epi, void* stream) {
+    return smc_conv3x3_wino_ws_f32(x, n, cin, h, w, y, cout, uw, s_in, epi, nullptr, 0, stream);
+}
+
+SMC_API int smc_conv3x3_wino_ws_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
+                                    const float* s_in, const smc_conv_epilogue* epi, float* workspace,
+                                    int64_t workspace_bytes, void* stream) {
     SMC_CHECK(x && y && uw, "smc_conv3x3_wino_f32: null pointer");
     if (!smc_conv3x3_wino_supported(n, cin, cout, h, w)) {
         smc::set_error("smc_conv3x3_wino_f32: no Winograd kernel for n=%d cin=%d cout=%d %dx%d", n, cin, cout, h, w);
@@ -535,6 +577,20 @@ SMC_API int smc_conv3x3_wino_f32(const float* x, int n, int cin, int h, int w, f
     const int64_t items = (int64_t)n * p.gx * p.gy * p.ntn;
     SMC_CHECK(items < (1LL << 31), "smc_conv3x3_wino_f32: grid too large");
     hipStream_t st = smc::as_stream(stream);
+    // split K when the caller passed the workspace smc_conv3x3_wino_workspace_size() asks for (without one: one
+    // workgroup per item over the whole K range, as before)
+    const int64_t need = smc_conv3x3_wino_workspace_size(n, cin, cout, h, w);
+    p.nsplit = 1;
+    if (need > 0 && workspace && workspace_bytes >= need) {
+        SMC_CHECK((reinterpret_cast<uintptr_t>(workspace) & 7) == 0, "smc_conv3x3_wino_ws_f32: workspace alignment");
+        p.nsplit = wino_nsplit(n, cin, cout, h, w);
+        p.split_stride = (int64_t)n * cout * h * w;
+        p.ws = workspace;
+        launch_wino_s<3>(s_in != nullptr, tc, p, items, st);
+        const int rc = smc::check_launch("smc_conv3x3_wino_ws_f32");
+        if (rc != SMC_OK) return rc;
+        return smc_modconv_epilogue_f32(workspace, p.nsplit, p.split_stride, y, n, cout, h, w, &e, stream);
+    }
     // the synthesis' two MODACT forms get an epilogue body with the activation fixed at compile time
     const bool modact_plain = p.mode == SMC_EPI_MODACT && !p.ext.residual;
     if (modact_plain && p.act == SMC_ACT_LRELU && p.alpha >= 0.f && p.alpha <= 1.f && p.clamp >= 0.f)

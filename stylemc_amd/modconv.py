@@ -144,14 +144,20 @@ def wino_ok(n, cin, cout, h, w):
     return WINOGRAD and bool(_hip.load().smc_conv3x3_wino_supported(n, cin, cout, h, w))
 
 
+# Split K for the grids of fewer than 512 work items (the 32 x 32 convs: smc_conv3x3_wino_workspace_size).
+WINO_SPLIT = True
+
+
 def wino(x, y, uw, cin, cout, s=None, epi=None, alg_flops=0.0, alg_bytes=0):
     """One smc_conv3x3_wino_f32 launch (3x3, stride 1, pad 1).  alg_flops: the MFMA FLOPs it executes
     (16 / 36 of the direct conv's; the timer also records the direct-equivalent count)."""
     n, _, h, w = x.shape
+    ws_bytes = _hip.load().smc_conv3x3_wino_workspace_size(n, cin, cout, h, w) if WINO_SPLIT else 0
+    ws = torch.empty(ws_bytes // 4, device=x.device, dtype=torch.float32) if ws_bytes > 0 else None
     tm = _hip.timer()
     tok = tm.wrap(alg_flops, alg_bytes, kind="wino", equiv_flops=alg_flops * 36 / 16) if tm is not None else None
-    _hip.call("smc_conv3x3_wino_f32", x.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(), _hip.ptr(s),
-              ctypes.byref(epi) if epi is not None else None, _hip.stream())
+    _hip.call("smc_conv3x3_wino_ws_f32", x.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(), _hip.ptr(s),
+              ctypes.byref(epi) if epi is not None else None, _hip.ptr(ws), ws_bytes, _hip.stream())
     if tok is not None:
         tm.finish(tok)
 

@@ -293,12 +293,12 @@ def _misaligned(t):
     return v
 
 
-@pytest.mark.parametrize("n,c,h", [(2, 8, 64), (1, 4, 37), (2, 3, 256)])
+@pytest.mark.parametrize("n,c,h", [(2, 8, 64), (1, 4, 37), (2, 3, 256), (1, 2, 100)])
 def test_blur_act_load_paths(n, c, h):
     """conv0's fused FIR + modconv epilogue (smc_modconv_blur_act_f32) and its backward: the 16-B load kernels
     (16-B aligned buffers; any T row pitch, incl. the transposed conv's odd 2h + 1 and an explicit padded pitch)
     against the scalar-load kernels (a misaligned copy of the same buffers) -- the same FIR arithmetic, so y, u and
-    dT must agree bit for bit (dd: block sums in a different atomic order, 1e-6) -- and U against fp64 torch."""
+    dT must agree bit for bit (dd: block sums in a different atomic order, 4e-6 of the max) -- and U against fp64 torch."""
     import ctypes
     import torch.nn.functional as F
     from stylemc_amd import _hip, modconv
@@ -359,7 +359,7 @@ def test_blur_act_load_paths(n, c, h):
     torch.cuda.synchronize()
     assert torch.isfinite(dt0).all()
     assert torch.equal(dt0, dt1), "dT scalar vs 16-B loads"
-    close(dd0, dd1, 1e-6, "dd")
+    close(dd0, dd1, 4e-6, "dd")  # ~30 block partials per plane at 200 px, added by atomics in any order
     # y = epi_y(u) bit for bit, so the mask and dT are identical
     assert torch.equal(dt2, dt0), "dT from y vs from u"
     assert torch.equal(dt3, dt0), "dT from y, scalar loads"

@@ -156,6 +156,65 @@ def test_wino_modact_epilogue_vs_direct_gemm():
     assert ((yw - yd).norm() / yd.norm()).item() <= 1e-6
 
 
+SPLIT_SHAPES = [  # grids under 512 work items: the split-K form (K splits of >= 8 steps)
+    (2, 512, 512, 32, 32),   # 128 items, 4 splits
+    (4, 512, 512, 32, 32),   # the FFHQ-1024 batch-4 32 x 32 conv: 256 items, 2 splits
+    (1, 128, 96, 64, 256),   # 192 items, 2 splits (16 steps)
+]
+
+
+@pytest.mark.parametrize("shape", SPLIT_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_wino_split_k_vs_fp64(shape):
+    """smc_conv3x3_wino_ws_f32 with its workspace: K splits + the epilogue kernel's reduction, STORE vs fp64 and the
+    MODACT epilogue (demod, noise, bias, lrelu, gain, clamp, u store) vs the single-pass kernel."""
+    H = _lib()
+    lib = H.load()
+    n, cin, cout, h, w = shape
+    ws_bytes = lib.smc_conv3x3_wino_workspace_size(n, cin, cout, h, w)
+    assert ws_bytes > 0
+    g = torch.Generator().manual_seed(5 + sum(shape))
+    x = torch.randn(n, cin, h, w, generator=g)
+    s = torch.rand(n, cin, generator=g) + 0.5
+    W = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    xd, sd, Wd = x.to(DEV), s.to(DEV), W.to(DEV)
+    uw = torch.empty(16 * cin * cout, device=DEV)
+    H.call("smc_wino_weights_f32", Wd.data_ptr(), cout, cin, 0, uw.data_ptr(), H.stream())
+    ws = torch.full((ws_bytes // 4,), float("nan"), device=DEV)
+    y = torch.empty(n, cout, h, w, device=DEV)
+    H.call("smc_conv3x3_wino_ws_f32", xd.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(), sd.data_ptr(),
+           None, ws.data_ptr(), ws_bytes, H.stream())
+    torch.cuda.synchronize()
+    _check(y, x.double() * s.double()[:, :, None, None], W.double(), f"split fwd {shape}")
+
+    from stylemc_amd import modconv
+    d = (torch.rand(n, cout, generator=g) + 0.5).to(DEV)
+    noise = torch.randn(n, 1, h, w, generator=g).to(DEV)
+    strength = torch.tensor([0.3], device=DEV)
+    bias = torch.randn(cout, generator=g).to(DEV)
+    outs = []
+    for split in (True, False):
+        yy, uu = torch.empty(n, cout, h, w, device=DEV), torch.empty(n, cout, h, w, device=DEV)
+        epi = modconv._epilogue(H.EPI_MODACT, d, noise, h * w, strength, bias, "lrelu", 0.2, 2 ** 0.5, 1.5, uu)
+        H.call("smc_conv3x3_wino_ws_f32", xd.data_ptr(), n, cin, h, w, yy.data_ptr(), cout, uw.data_ptr(),
+               sd.data_ptr(), ctypes.byref(epi), ws.data_ptr() if split else None, ws_bytes if split else 0,
+               H.stream())
+        outs.append((yy, uu))
+    torch.cuda.synchronize()
+    (ys, us), (y1, u1) = outs
+    assert (us - u1).abs().max().item() <= 2e-5 * u1.abs().max().item()
+    assert (ys - y1).abs().max().item() <= 1e-4 * y1.abs().max().item()
+    assert ((ys - y1).norm() / y1.norm()).item() <= 1e-6
+
+
+def test_wino_split_plan():
+    lib = _lib().load()
+    assert lib.smc_conv3x3_wino_workspace_size(4, 512, 512, 32, 32) == 2 * 4 * 512 * 32 * 32 * 4
+    assert lib.smc_conv3x3_wino_workspace_size(2, 512, 512, 32, 32) == 4 * 2 * 512 * 32 * 32 * 4
+    assert lib.smc_conv3x3_wino_workspace_size(4, 512, 512, 64, 64) == 0     # 1024 items: one pass
+    assert lib.smc_conv3x3_wino_workspace_size(2, 32, 32, 32, 32) == 0       # 4 K steps: nothing to split
+    assert lib.smc_conv3x3_wino_workspace_size(1, 512, 512, 16, 16) == 0     # no kernel
+
+
 def test_wino_unsupported_shapes():
     H = _lib()
     lib = H.load()

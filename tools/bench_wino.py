@@ -33,11 +33,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--no-split", action="store_true", help="F(2x2) without split K (modconv.WINO_SPLIT off)")
+    ap.add_argument("--res", type=int, nargs="+", default=[32, 64, 128, 256, 512, 1024])
     args = ap.parse_args()
     build.build(verbose=False)
+    modconv.WINO_SPLIT = not args.no_split
     n, dev = args.batch, "cuda"
     tot = {"direct": 0.0, "wino": 0.0, "wino4": 0.0}
-    for r in [32, 64, 128, 256, 512, 1024]:
+    for r in args.res:
         c = min(32768 // r, 512)
         W = torch.randn(c, c, 3, 3, device=dev) / (3 * c ** 0.5)
         P = modconv.PackedConv(W, 1)
