@@ -133,7 +133,7 @@ class DirectionFinder:
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
                  overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None, G2=None, temp_shapes2=None,
-                 prefetch_id=True, prefetch_clip=False):
+                 prefetch_id=True, prefetch_clip=False, graph_prefetch=False):
         self.G = G
         # the edited image's generator (train_latent_mapper.py:100-106,159-162 --network2; default G itself)
         self.G_edit = G2 if G2 is not None else G
@@ -151,6 +151,15 @@ class DirectionFinder:
         self.prefetch_id = prefetch_id
         # ... and its CLIP embeddings (then CLIP too sees only the edited images on the critical path)
         self.prefetch_clip = prefetch_clip
+        # the prefetch (no-gradient synthesis + its loss features: ~200 launches, fixed shapes) replayed as a
+        # captured HIP graph: one host call instead of the launches' Python + ctypes enqueue, which bounded the
+        # step where the GPU ran ahead of the host (the low-resolution layers, the loss heads).  Two graphs with
+        # their own static outputs, used alternately: a replay never overwrites the image / features the previous
+        # iteration's losses and backward may still read.  Falls back to eager launches if capture fails.
+        # Off: measured slower, 19.36-19.45 against 18.69-18.76 ms / step eager (profiles/r03_graph_prefetch_ab.txt).
+        self.graph_prefetch = graph_prefetch
+        self._graphs = {}
+        self._graph_flip = 0
         self._next_i = None
         self._pref = None
         # edited + original image through each loss network as ONE batch (backward for the edited half)
@@ -348,11 +357,50 @@ class DirectionFinder:
             self._pre = self.stream_factory(self.device)
         self._pre.wait_event(self._fwd_done)
         with torch.cuda.stream(self._pre), torch.no_grad():
-            orig = self.synth_fn(self.G, self.until_k, self.styles_array[a:b], self.temp_shapes, self.noise_mode)
-            feats = self.id_loss.target_feats(orig) if self.prefetch_id else None
-            embs = ([cl.encode_src(s) for (cl, _), (_, s) in zip(self.clip_losses, self._clip_inputs(None, orig))]
-                    if self.prefetch_clip else None)
-        self._pref = ((a, b), orig, feats, embs)
+            out = self._graph_replay(self.styles_array[a:b]) if self.graph_prefetch else None
+            if out is None:
+                out = self._prefetch_body(self.styles_array[a:b])
+        self._pref = ((a, b),) + out
+
+    def _prefetch_body(self, styles):
+        orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
+        feats = self.id_loss.target_feats(orig) if self.prefetch_id else None
+        embs = ([cl.encode_src(s) for (cl, _), (_, s) in zip(self.clip_losses, self._clip_inputs(None, orig))]
+                if self.prefetch_clip else None)
+        return orig, feats, embs
+
+    def _graph_replay(self, styles):
+        """The prefetch body as a HIP graph replay on the current (prefetch) stream; captured on first use per
+        batch shape, two instances alternating.  None: capture failed (eager from then on)."""
+        key = (tuple(styles.shape), self._graph_flip)
+        self._graph_flip ^= 1
+        ent = self._graphs.get(key)
+        if ent is None:
+            try:
+                ent = self._graph_capture(styles)
+            except Exception as exc:  # a non-capturable op on this path: stay eager
+                warnings.warn(f"find_direction: prefetch graph capture failed ({exc}); eager prefetch")
+                self.graph_prefetch = False
+                return None
+            self._graphs[key] = ent
+        g, static_in, out = ent
+        static_in.copy_(styles)
+        g.replay()
+        return out
+
+    def _graph_capture(self, styles):
+        cur = torch.cuda.current_stream()
+        static_in = styles.clone()
+        cap = torch.cuda.Stream(device=styles.device)
+        cap.wait_stream(cur)
+        with torch.cuda.stream(cap):
+            self._prefetch_body(static_in)   # warm-up: lazily built state (packed weights, workspaces) first
+            cap.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap):
+                out = self._prefetch_body(static_in)
+        cur.wait_stream(cap)
+        return g, static_in, out
 
     def step(self):
         self.it += 1
