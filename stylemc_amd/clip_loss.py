@@ -26,6 +26,39 @@ from . import clip_model, synthetic, vit_hip
 
 MODEL_NAMES = {"small": "ViT-B/32", "large": "ViT-B/16"}
 
+# The loss head as one autograd node whose gradient is formed in the forward pass (module switch for A/B): autograd's
+# graph of the head (difference, norm, division, cosine_similarity, 1 - x) replays ~28 small kernels in the backward
+# on the step's critical path, between the CLIP forward and its backward; here the backward is one multiply.
+FUSED_HEAD = True
+
+
+class _DirectionHead(torch.autograd.Function):
+    """1 - cos(normalize(e - src), t) per sample, t unit-norm.  Forward: the reference's ops (same values).  Backward:
+    d/de = (cos u - t) / |e - src| per sample with u = normalize(e - src) -- the exact gradient of the formula up to
+    |u| = |t| = 1 (each within a few ulp in fp32), against autograd through cosine_similarity's own normalisation."""
+
+    @staticmethod
+    def forward(ctx, e, src, t):
+        f = e - src
+        nf = f.norm(dim=1, keepdim=True)
+        u = f / nf
+        cos = F.cosine_similarity(u, t)
+        ctx.save_for_backward(torch.addcmul(-t, cos[:, None], u) / nf)
+        return 1 - cos
+
+    @staticmethod
+    def backward(ctx, g):
+        (gf,) = ctx.saved_tensors
+        return g[:, None] * gf, None, None
+
+
+def direction_loss(e, src, t):
+    if FUSED_HEAD and e.requires_grad:
+        return _DirectionHead.apply(e, src, t)
+    f = e - src
+    f = f / f.norm(dim=1, keepdim=True)
+    return 1 - F.cosine_similarity(f, t)
+
 
 def split_clip_state_dict(sd):
     """OpenAI CLIP model state_dict -> (visual state_dict without the 'visual.' prefix, text state_dict)."""
@@ -78,9 +111,7 @@ class CLIPLoss(nn.Module):
         return self.visual(src_image)
 
     def per_sample_with(self, src_emb, tgt_image):
-        f = self.visual(tgt_image) - src_emb
-        f = f / f.norm(dim=1, keepdim=True)
-        return 1 - F.cosine_similarity(f, self.text_features)
+        return direction_loss(self.visual(tgt_image), src_emb, self.text_features)
 
     def per_sample_pair(self, tgt_image, src_image):
         """per_sample(src, tgt) with both images in ONE tower batch [tgt; src]: the backward runs for the
@@ -88,9 +119,7 @@ class CLIPLoss(nn.Module):
         n = tgt_image.shape[0]
         x = torch.cat([tgt_image, src_image.detach()])
         e = self.visual(x, n_grad=n) if getattr(self.visual, "supports_partial_grad", False) else self.visual(x)
-        f = e[:n] - e[n:].detach()
-        f = f / f.norm(dim=1, keepdim=True)
-        return 1 - F.cosine_similarity(f, self.text_features)
+        return direction_loss(e[:n], e[n:].detach(), self.text_features)
 
     def per_sample(self, src_image, tgt_image):
         return self.per_sample_with(self.encode_src(src_image), tgt_image)

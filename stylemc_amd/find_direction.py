@@ -126,6 +126,41 @@ def cosine_lr(lr0, it, total):
     return float(np.cos(np.pi * it / total) * lr0 * 0.5 + lr0 * 0.5)
 
 
+# The loss composition (find_direction.py:318-330: coefficients x batch sums + the l2 term) as one autograd node with
+# an analytic backward (module switch for A/B): autograd's graph of those scalar ops replays ~20 tiny kernels between
+# the loss heads and the networks' backward, on the step's critical path.
+FUSED_TOTAL = True
+
+
+class _LossTotal(torch.autograd.Function):
+    """Forward: the reference's composition op for op (same values); returns (total, parts = [clip, id, 0, l2]).
+    Backward: d total / d id_terms = c_id / denom, d / d clip_terms = c_clip / denom and
+    d / d d = 2 ((sT + d) - sT) c_l2 / l2_den -- the derivative autograd forms, in one multiply each."""
+
+    @staticmethod
+    def forward(ctx, id_terms, clip_terms, d, sT, c_id, c_clip, c_l2, l2_den, denom):
+        diff = (sT + d) - sT
+        l2_sum = diff.square().sum()
+        id_part = c_id * id_terms.sum() / denom
+        clip_part = c_clip * clip_terms.sum() / denom
+        l2_part = c_l2 * l2_sum / l2_den
+        parts = torch.stack([clip_part, id_part, torch.zeros_like(l2_part), l2_part])
+        ctx.mark_non_differentiable(parts)
+        ctx.save_for_backward(diff)
+        ctx.k = (c_id / denom, c_clip / denom, 2.0 * c_l2 / l2_den)
+        ctx.shapes = (id_terms.shape, clip_terms.shape)
+        return id_part + clip_part + l2_part, parts
+
+    @staticmethod
+    def backward(ctx, g, _gparts):
+        (diff,) = ctx.saved_tensors
+        k_id, k_clip, k_l2 = ctx.k
+        gid = (g * k_id).expand(ctx.shapes[0]) if ctx.needs_input_grad[0] else None
+        gclip = (g * k_clip).expand(ctx.shapes[1]) if ctx.needs_input_grad[1] else None
+        gd = diff * (g * k_l2) if ctx.needs_input_grad[2] else None
+        return gid, gclip, gd, None, None, None, None, None, None
+
+
 class DirectionFinder:
     """State of one find_direction run; ``step()`` is one iteration of the reference's hot loop."""
 
@@ -328,6 +363,11 @@ class DirectionFinder:
     def _finish(self, styles, d, id_terms, clip_terms, denom):
         T = S_TRAINABLE_SPACE_CHANNELS
         sT = styles.index_select(1, self.t_idx)
+        if FUSED_TOTAL:
+            total, parts = _LossTotal.apply(id_terms, clip_terms, d, sT, self.coef["id"], self.coef["clip"],
+                                            self.coef["l2"], float(denom * len(T) * 512), float(denom))
+            (g,) = torch.autograd.grad(total, d)
+            return g, parts
         l2_sum = ((sT + d) - sT).square().sum()
         id_part = self.coef["id"] * id_terms.sum() / denom
         clip_part = self.coef["clip"] * clip_terms.sum() / denom

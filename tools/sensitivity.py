@@ -69,10 +69,14 @@ def main():
     variants = {"default": (clip, idl, {}), "no_clip": ([(free, 1.0)], idl, {}), "no_irse": (clip, free, {}),
                 "no_losses": ([(free, 1.0)], free, {}), "no_prefetch": (clip, idl, dict(prefetch_orig=False)),
                 "irse_pair": (clip, idl, dict(prefetch_id=False)), "clip_pref": (clip, idl, dict(prefetch_clip=True)),
-                "side_hi": (clip, idl, {}), "graph": (clip, idl, dict(graph_prefetch=True)),
+                "side_hi": (clip, idl, {}), "graph": (clip, idl, dict(graph_prefetch=True)), "unfused": (clip, idl, {}),
                 "main_side_hi": (clip, idl, {})}
     name = sys.argv[sys.argv.index("--variant") + 1]
     clips, idloss, kw = variants[name]
+    if name == "unfused":  # the loss head and composition through autograd's op-by-op graph
+        from stylemc_amd import clip_loss
+        clip_loss.FUSED_HEAD = False
+        FD.FUSED_TOTAL = False
     f = finder(clips, idloss, **kw)
     # stream priority variants: the IR-SE50 (side) stream -- or it and the main stream (edited synthesis, CLIP,
     # backward) -- at high priority; the prefetch stream (next iteration's original image) stays normal
