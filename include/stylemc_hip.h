@@ -155,8 +155,8 @@ int smc_wino_weights_f32(const float* w, int cout, int cin, int flip, float* uw,
 /* Winograd F(4x4, 3x3) form of the same convolution (4x4 output tiles, 36 multiplies per channel pair instead of
  * 144; interpolation points 0, +-1, +-2), same operands and epilogue semantics as smc_conv3x3_wino_f32 and the same
  * C-ABI contract (replaces the same grouped conv2d of conv2d_resample.py:147-154).  uw holds the taps written by
- * smc_wino4_weights_f32.  smc_conv3x3_wino4_supported(): cin % 4, w % 64 == 0, and cout % 64 with h % 8 or
- * cout % 32 with h % 16; input < 2 GiB.  x, y, uw, u_save and noise 16-B aligned (noise_nstride % 4 == 0). */
+ * smc_wino4_weights_f32.  smc_conv3x3_wino4_supported(): cin % 4 == 0, w % 64 == 0, h % 8 == 0, cout % 64 == 0;
+ * input and taps < 2 GiB.  x, y, uw, u_save and noise 16-B aligned (noise_nstride % 4 == 0). */
 int smc_conv3x3_wino4_supported(int n, int cin, int cout, int h, int w);
 int smc_conv3x3_wino4_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
                           const float* s_in, const smc_conv_epilogue* epi, void* stream);
