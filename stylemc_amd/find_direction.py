@@ -168,7 +168,7 @@ class DirectionFinder:
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
                  overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None, G2=None, temp_shapes2=None,
-                 prefetch_id=True, prefetch_clip=False, graph_prefetch=False):
+                 prefetch_id=True, prefetch_clip=False, graph_prefetch=False, prefetch_after="forward"):
         self.G = G
         # the edited image's generator (train_latent_mapper.py:100-106,159-162 --network2; default G itself)
         self.G_edit = G2 if G2 is not None else G
@@ -193,6 +193,12 @@ class DirectionFinder:
         # iteration's losses and backward may still read.  Falls back to eager launches if capture fails.
         # Off: measured slower, 19.36-19.45 against 18.69-18.76 ms / step eager (profiles/r03_graph_prefetch_ab.txt).
         self.graph_prefetch = graph_prefetch
+        # where the prefetch may start on the GPU: "forward" (after this iteration's edited forward: beside the
+        # latency-bound loss networks and the backward), "losses" (after the loss networks' forward: beside the
+        # backward only) or "none" (as soon as it is enqueued)
+        assert prefetch_after in ("forward", "losses", "none"), prefetch_after
+        self.prefetch_after = prefetch_after
+        self._loss_done = None
         self._graphs = {}
         self._graph_flip = 0
         self._next_i = None
@@ -363,6 +369,9 @@ class DirectionFinder:
     def _finish(self, styles, d, id_terms, clip_terms, denom):
         T = S_TRAINABLE_SPACE_CHANNELS
         sT = styles.index_select(1, self.t_idx)
+        if self.prefetch_after == "losses" and d.is_cuda:
+            self._loss_done = torch.cuda.Event()
+            self._loss_done.record(torch.cuda.current_stream())
         if FUSED_TOTAL:
             total, parts = _LossTotal.apply(id_terms, clip_terms, d, sT, self.coef["id"], self.coef["clip"],
                                             self.coef["l2"], float(denom * len(T) * 512), float(denom))
@@ -395,7 +404,10 @@ class DirectionFinder:
             return
         if getattr(self, "_pre", None) is None:
             self._pre = self.stream_factory(self.device)
-        self._pre.wait_event(self._fwd_done)
+        if self.prefetch_after == "forward":
+            self._pre.wait_event(self._fwd_done)
+        elif self.prefetch_after == "losses" and self._loss_done is not None:
+            self._pre.wait_event(self._loss_done)
         with torch.cuda.stream(self._pre), torch.no_grad():
             out = self._graph_replay(self.styles_array[a:b]) if self.graph_prefetch else None
             if out is None:
