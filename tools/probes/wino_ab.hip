@@ -89,7 +89,7 @@ int run(int r, bool with_s, double* tot) {
     hipLaunchKernelGGL(fill_kernel, dim3(16), dim3(256), 0, 0, s, (size_t)n * c, 3u, 1.f, 1.f);
     WinoParams p{};
     p.x = x; p.n = n; p.cin = c; p.h = r; p.w = r; p.cout = c; p.uw = uw; p.s = with_s ? s : nullptr;
-    p.mode = SMC_EPI_STORE; p.act = SMC_ACT_LINEAR; p.gain = 1.f; p.clamp = -1.f;
+    p.mode = SMC_EPI_STORE; p.act = SMC_ACT_LINEAR; p.gain = 1.f; p.clamp = -1.f; p.nsplit = 1;
     p.ext.rs = 1;
     const double flops = 2.0 * n * c * c * (r / 2) * (r / 2) * 16;
     p.y = y0;
