@@ -53,7 +53,7 @@ class _DirectionHead(torch.autograd.Function):
 
 
 def direction_loss(e, src, t):
-    if FUSED_HEAD and e.requires_grad:
+    if FUSED_HEAD and e.requires_grad and not src.requires_grad and not t.requires_grad:
         return _DirectionHead.apply(e, src, t)
     f = e - src
     f = f / f.norm(dim=1, keepdim=True)
