@@ -470,9 +470,12 @@ __global__ __launch_bounds__(256) void wino_weights_kernel(const float* w, int c
 }
 
 // tile columns of a workgroup's block: 64, 32 or 16 (the kernel's instantiations), dividing the tile grid
+#ifndef SMC_WINO_TC_MAX
+#define SMC_WINO_TC_MAX 64
+#endif
 int wino_tc(int h, int w) {
     if (h % 2 || w % 4 || w < 32) return 0;
-    for (int tc = 64; tc >= 16; tc /= 2)
+    for (int tc = SMC_WINO_TC_MAX; tc >= 16; tc /= 2)
         if ((w / 2) % tc == 0 && (h / 2) % (WBT / tc) == 0) return tc;
     return 0;
 }
