@@ -5,6 +5,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+With no launcher in the environment (no WORLD_SIZE), ``--gpus N > 1`` starts the N rank processes itself
+(spawn_ranks: fresh processes, before any GPU call here).  Under a launcher, a WORLD_SIZE that differs from
+--gpus exits with status 2.  One-GPU rehearsal of the N-rank path: SMC_SHARE_GPU=1 SMC_DIST_BACKEND=gloo
+(every rank on device 0; RCCL refuses two ranks on one GPU) -- the line then says ranks_share_gpu, and its
+throughput is not a scaling number.
+
 A step = one find_direction iteration (find_direction.py:292-347) on synthetic inputs that are
 resident in HBM before timing: a config-f FFHQ-1024 generator with seeded weights, S codes
 [129, 26, 512] ~ N(1, 0.5), seeded CLIP ViT-B/32 + IR-SE50, --clip_type small, landmarks 0.
@@ -51,6 +57,7 @@ METRIC = "find_direction images/sec @ FFHQ-1024 bs=4, 1/2/4/8 GPU; dir cosine-si
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--resolution", type=int, default=1024)
@@ -230,8 +237,66 @@ def pmc_traffic():
     return d.get("conv_gemm_bytes_per_launch"), src
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` with no launcher in the environment: start N fresh rank processes of this same
+    command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run would) and return the first
+    non-zero exit status, else 0.  Runs before this process makes any GPU call (torch.cuda.device_count() does
+    not initialise the GPU on this image), so the children are started from a GPU-free parent.  A rank that
+    fails ends the others (their exact PIDs), so a dead rank cannot leave its peers waiting in a collective."""
+    import subprocess
+    visible = torch.cuda.device_count()
+    share = os.environ.get("SMC_SHARE_GPU") == "1"
+    if visible < n and not share:
+        print(f"bench.py: --gpus {n} but {visible} GPU(s) visible; set SMC_SHARE_GPU=1 SMC_DIST_BACKEND=gloo for a "
+              f"one-GPU rehearsal", file=sys.stderr)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SMC_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return status
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher but --gpus {args.gpus}",
+                  file=sys.stderr)
+            sys.exit(2)
+    elif args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.launch_probe:   # launcher test (tests/test_bench_launcher_cpu.py): report the rank environment, no GPU
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "SMC_BENCH_LAUNCHER")
+        print(json.dumps({k: os.environ.get(k) for k in keys}), flush=True)
+        sys.exit(int(os.environ.get("SMC_PROBE_FAIL_RANK", "-1")) == int(os.environ.get("RANK", "0")) and 3 or 0)
     from stylemc_amd import _hip, build
     from stylemc_amd import dist as sdist
     world = sdist.init_from_env(use_cuda=True)
@@ -366,7 +431,10 @@ def main():
                    "n_seeds": n_seeds, "seeds_per_gpu": n_seeds / world.world_size,
                    "parallelism": f"dp{world.world_size}", "clip_type": args.clip_type, "clip_impl": args.clip_impl, "id_impl": args.id_impl,
                    "batched_loss_pairs": finder.batch_losses, "landmarks_loss_coef": 0,
-                   "direction_finite": finite},
+                   "direction_finite": finite, "world_size": world.world_size, "backend": world.backend,
+                   "launcher": (os.environ.get("SMC_BENCH_LAUNCHER", "torch.distributed.run")
+                                if world.world_size > 1 else None),
+                   "ranks_share_gpu": world.world_size > 1 and os.environ.get("SMC_SHARE_GPU") == "1"},
         "roofline": roofline,
         "cpu_baseline": None,
         "parity": None,

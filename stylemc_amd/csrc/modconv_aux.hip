@@ -681,6 +681,44 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const float* g, const floa
     }
 }
 
+// dd[n, o] += sum_hw dz * u with ONE workgroup per plane (fixed thread strides, fixed reduction tree): the style
+// gradient of the demodulation is then bit-reproducible whatever the plane size.  The fused act / FIR backward
+// kernels add their per-tile partials with float atomics, which is order-independent only while a plane has at most
+// two dd-owning tiles (two addends onto zero commute) -- true for every trainable layer of find_direction (b8..b64);
+// larger planes run those kernels without dd and this pass after them (dd_planes_need_pass).
+__global__ __launch_bounds__(256) void dd_plane_kernel(const float* g, const float* u, float* dd, int c, int64_t hw,
+                                                       Epi e) {
+    __shared__ float red[4];
+    const int64_t nc = blockIdx.x;
+    const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
+    const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
+    const float dv = e.d ? e.d[nc] : 1.f;
+    const float bv = e.bias ? e.bias[o] : 0.f;
+    const float* gp = g + nc * hw;
+    const float* up = u + nc * hw;
+    const float* np_ = e.noise ? e.noise + n * e.noise_nstride : nullptr;
+    float part[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t p0 = threadIdx.x; p0 < hw; p0 += 256 * 4) {
+        float uv[4], gv[4], nv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t p = p0 + 256 * k;
+            const int64_t pp = p < hw ? p : 0;
+            uv[k] = up[pp];
+            gv[k] = gp[pp];
+            nv[k] = np_ ? np_[pp] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (p0 + 256 * k >= hw) continue;
+            const float yv = smc::epi_y(uv[k], dv, nv[k] * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
+            part[k] += smc::act_grad_y(e.act, gv[k], yv, e.alpha, e.gain, e.clamp) * uv[k];
+        }
+    }
+    const float tot = block_sum256((part[0] + part[1]) + (part[2] + part[3]), red);
+    if (threadIdx.x == 0) dd[nc] += tot;
+}
+
 // float4 form (hw % 4 == 0): each thread owns AB_V float4 groups of one plane, all loads issued first.
 constexpr int AB_V = 4;
 template <bool FROMY>
@@ -891,7 +929,16 @@ SMC_API int smc_modconv_act_bwd_f32(const float* g, const float* u, float* du, f
     SMC_CHECK(planes < 65536, "smc_modconv_act_bwd_f32: too many planes");
     const uintptr_t align = (uintptr_t)g | (uintptr_t)u | (uintptr_t)du | (uintptr_t)(from_y ? nullptr : epi->noise);
     hipStream_t st = smc::as_stream(stream);
-    if (hw % 4 == 0 && (from_y || !epi->noise || epi->noise_nstride % 4 == 0) && align % 16 == 0) {
+    const bool vec4 = hw % 4 == 0 && (from_y || !epi->noise || epi->noise_nstride % 4 == 0) && align % 16 == 0;
+    // more than two workgroups per plane: dd from the one-workgroup-per-plane pass (deterministic order)
+    const int64_t blocks_per_plane = vec4 ? smc::ceil_div(hw / 4, 256 * AB_V) : std::max<int64_t>(1, smc::ceil_div(hw, 256 * 8));
+    if (dd && blocks_per_plane > 2) {
+        const int rc = smc_modconv_act_bwd_f32(g, u, du, nullptr, n, c, h, w, epi, stream);
+        if (rc != SMC_OK) return rc;
+        hipLaunchKernelGGL(dd_plane_kernel, dim3((unsigned)planes), dim3(256), 0, st, g, u, dd, c, hw, to_epi(epi));
+        return smc::check_launch("smc_modconv_act_bwd_f32 (dd)");
+    }
+    if (vec4) {
         const dim3 grid((unsigned)smc::ceil_div(hw / 4, 256 * AB_V), (unsigned)planes);
         if (from_y) hipLaunchKernelGGL(act_bwd_vec4_kernel<true>, grid, dim3(256), 0, st, g, u, du, dd, c, hw, to_epi(epi));
         else hipLaunchKernelGGL(act_bwd_vec4_kernel<false>, grid, dim3(256), 0, st, g, u, du, dd, c, hw, to_epi(epi));
@@ -948,6 +995,16 @@ SMC_API int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* 
     const bool from_y = epi->grad_from_y != 0;
     SMC_CHECK(!from_y || !dd, "smc_modconv_blur_act_bwd_f32: dd needs u (grad_from_y set)");
     hipStream_t st = smc::as_stream(stream);
+    // dd-owning tiles per plane (each tile owns its 32 x 64 window of the u plane): more than two -> the fused kernel
+    // runs without dd and the one-workgroup-per-plane pass adds it (deterministic order)
+    if (dd && smc::ceil_div(u_h, kFH) * smc::ceil_div(u_w, kFW) > 2) {
+        const int rc = smc_modconv_blur_act_bwd_f32(g, u, dt, nullptr, n, c, u_h, u_w, t_h, t_w, t_pitch, f, fh, fw,
+                                                    padx0, pady0, fgain, flip, epi, stream);
+        if (rc != SMC_OK) return rc;
+        hipLaunchKernelGGL(dd_plane_kernel, dim3((unsigned)((int64_t)n * c)), dim3(256), 0, st, g, u, dd, c,
+                           (int64_t)u_h * u_w, to_epi(epi));
+        return smc::check_launch("smc_modconv_blur_act_bwd_f32 (dd)");
+    }
     const dim3 grid = fir_grid_bwd((int64_t)n * c, t_w, t_h);
     const Epi e = to_epi(epi);
     const uintptr_t al = (uintptr_t)g | (uintptr_t)u | (uintptr_t)(from_y ? nullptr : epi->noise);

@@ -472,9 +472,9 @@ __global__ __launch_bounds__(256) void wino_weights_kernel(const float* w, int c
 // tile columns of a workgroup's block: 64, 32 or 16 (the kernel's instantiations), dividing the tile grid
 // Tile columns per block, at most (A/B knob).  A cap of 32 (2 tile rows at W >= 64) measured 477 / 468 against
 // 480 / 473 us at r = 1024 fwd / data grad and 18.64-18.70 against 18.72-18.74 ms per step over three interleaved
-// rounds (profiles/r03_wino_tc_ab.txt); not switched this round (the GPU pool was unavailable for its test run).
+// rounds (profiles/r03_wino_tc_ab.txt); the default since round 4.
 #ifndef SMC_WINO_TC_MAX
-#define SMC_WINO_TC_MAX 64
+#define SMC_WINO_TC_MAX 32
 #endif
 int wino_tc(int h, int w) {
     if (h % 2 || w % 4 || w < 32) return 0;

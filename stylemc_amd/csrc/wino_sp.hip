@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * HW * 4), 0x00020000);
     const __amdgpu_buffer_rsrc_t ursrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.uw, (short)0, p.cin * 16 * p.cout * 4, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.uw, (short)0, (int)((int64_t)p.cin * 16 * p.cout * 4), 0x00020000);
     // U lanes: run = channel * 4 + xi group (32 x 16 B each), 2 runs per wave-instruction
     int uv[UJW];
 #pragma unroll
@@ -295,6 +295,7 @@ SMC_API int smc_wino_sp_supported(int n, int cin, int cout, int h, int w) {
     if (n < 1 || cin < 2 * SBK || cin % SBK || cout < SBO || cout % SBO) return 0;
     if (h < 2 || w < 2 || h > 16 || w > 16) return 0;
     if ((int64_t)n * cin * h * w * 4 >= (1LL << 31)) return 0;
+    if ((int64_t)cin * 16 * cout * 4 >= (1LL << 31)) return 0;   // the U slab's buffer range (num_records)
     return 1;
 }
 

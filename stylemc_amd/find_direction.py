@@ -357,7 +357,8 @@ class DirectionFinder:
             img = self._synth_edited(styles, d)
             main.wait_stream(side)
             for t in [y_feats] + src_embs:
-                t.record_stream(main)
+                if t is not None:   # NadaTerms.encode_src: None when no term needs the source image
+                    t.record_stream(main)
         else:
             img = self._synth_edited(styles, d)
             y_feats, src_embs = self._original_branch(styles)

@@ -1,0 +1,77 @@
+"""One rank of the multi-rank GPU find_direction test (tests/test_gpu_distributed.py).
+
+    RANK=r WORLD_SIZE=n MASTER_ADDR=127.0.0.1 MASTER_PORT=p SMC_DIST_BACKEND=gloo SMC_SHARE_GPU=1 \
+        python -m tests.dist_gpu_worker OUT.npz
+
+Runs `run_cases` (the same DirectionFinder problems the test runs single-process) with the default three-stream
+schedule -- edited synthesis on the main stream, IR-SE50 beside CLIP on the side stream, the next iteration's
+original image prefetched on the third stream -- and the rank's shard of every global batch; rank 0 writes the
+results.  Started as a fresh process (never forked from a process that touched the GPU).
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+# (global batch, S codes, steps): even shards (4 over 8), uneven 2 + 1 with a short last batch of 1 that leaves
+# rank 1 empty (3 over 7), and rank 1 empty on every step (1 over 3)
+CASES = ((4, 8, 3), (3, 7, 4), (1, 3, 3))
+RES = 256
+
+
+def problem(dev):
+    from stylemc_amd import networks, synthetic
+    from stylemc_amd.clip_loss import CLIPLoss
+    from stylemc_amd.id_loss import IDLoss
+    cfg = synthetic.generator_config(resolution=RES)
+    G = networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=dev)
+    text = synthetic.text_direction("a photo of a face of a feminine woman", "a photo of a face of a man")
+    clip = [(CLIPLoss(dev, text_features=text, synthetic_weights=True, seed=4), 1.0)]
+    return G, clip, IDLoss(device=dev, weights=None, seed=3)
+
+
+def run_cases(world, dev, G, clip, idl):
+    from stylemc_amd import synthetic
+    from stylemc_amd.find_direction import DirectionFinder, initial_delta
+    out = {}
+    for gb, n_items, steps in CASES:
+        styles = synthetic.synthetic_styles(n_items, seed=5).to(dev)
+        f = DirectionFinder(G, styles, clip, idl, resolution=RES, batch_size=gb, global_batch=gb, n_epochs=4,
+                            seed=1, world=world, init_delta=initial_delta(0, 0.01))
+        assert f.prefetch_orig and f.batch_losses and f._side_stream() is not None, "not the pipelined schedule"
+        parts, picks = [], []
+        for _ in range(steps):
+            last = f.step()
+            parts.append(last["parts"].cpu())
+            picks.append(last["batch"])
+        torch.cuda.synchronize()
+        out[f"delta_{gb}"] = f.delta.cpu().numpy()
+        out[f"sdir_{gb}"] = f.styles_direction.cpu().numpy()
+        out[f"parts_{gb}"] = torch.stack(parts).numpy()
+        out[f"picks_{gb}"] = np.array(picks)
+    return out
+
+
+def main(path):
+    from stylemc_amd import _hip, build
+    from stylemc_amd import dist as sdist
+    world = sdist.init_from_env(use_cuda=True)
+    dev = torch.device("cuda", world.device_index)
+    build.build(verbose=False) if world.rank == 0 else None
+    world.barrier()
+    _hip.load()
+    out = run_cases(world, dev, *problem(dev))
+    world.barrier()
+    if world.rank == 0:
+        out["world_size"] = np.array(world.world_size)
+        np.savez(path, **out)
+    torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
