@@ -7,7 +7,8 @@ Run here (the container that has /root/reference), never on the GPU box:
 What is imported from the reference (read-only, CPU, its pure-torch ``_ref`` paths):
   torch_utils.ops.upfirdn2d / bias_act / conv2d_resample / fma, utils.block_forward /
   utils.generate_image / utils.get_temp_shapes (with a stub ``cv2`` module: cv2 is only used by the
-  blending helpers), id_loss.model_irse.Backbone.
+  blending helpers), id_loss.model_irse.Backbone, legacy.convert_tf_generator (with the oracle Generator standing
+  in for the absent training.networks).
 The StyleGAN2 layer classes are not in the reference tree; the tiny
 generator below evaluates the upstream ``modulated_conv2d`` formula on top of the reference's ops,
 so the fixture pins the reference ops + the reference block driver, with the layer formula restated.
@@ -801,9 +802,97 @@ def gen_mapper_train():
         "param_names": np.array([n for n, _ in mapper.named_parameters()])})
 
 
+# ---------------------------------------------------------------------------------- TF-era network pickles
+
+
+def tf_generator_tree():
+    """A seeded synthetic TensorFlow-era StyleGAN2 G (the dnnlib.tflib Network state: version, static_kwargs, own
+    variables, components): the config-f skip architecture at 32 px with fmap_base 256 and fmap_max 64 (channels
+    64 / 64 / 32 / 16: every width the HIP kernels take), a 32-wide latent and 2 mapping layers so the fixture stays
+    small.  Returns {component: [(name, array)]} with
+    component '' (G: dlatent_avg), 'mapping', 'synthesis', and the static kwargs."""
+    rng = np.random.RandomState(31)
+    kw = dict(latent_size=32, dlatent_size=32, label_size=0, resolution=32, num_channels=3, mapping_layers=2,
+              fmap_base=256, fmap_max=64, truncation_psi=0.5)
+    R, zd, wd = 32, 32, 32
+    ch = {r: min(kw["fmap_base"] * 2 // r, kw["fmap_max"]) for r in (4, 8, 16, 32)}
+
+    def a(*shape):
+        return rng.standard_normal(shape).astype(np.float32)
+
+    mapping = []
+    for i in range(kw["mapping_layers"]):
+        mapping += [(f"Dense{i}/weight", a(zd if i == 0 else wd, wd)), (f"Dense{i}/bias", a(wd))]
+    syn = [("4x4/Const/const", a(1, ch[4], 4, 4))]
+
+    def layer(prefix, cin, cout, k=3):
+        return [(f"{prefix}/weight", a(k, k, cin, cout)), (f"{prefix}/mod_weight", a(wd, cin)),
+                (f"{prefix}/mod_bias", a(cin)), (f"{prefix}/bias", a(cout))]
+
+    syn += layer("4x4/Conv", ch[4], ch[4]) + [("4x4/Conv/noise_strength", a())]
+    syn += layer("4x4/ToRGB", ch[4], 3, k=1)
+    for r in (8, 16, 32):
+        syn += layer(f"{r}x{r}/Conv0_up", ch[r // 2], ch[r]) + [(f"{r}x{r}/Conv0_up/noise_strength", a())]
+        syn += layer(f"{r}x{r}/Conv1", ch[r], ch[r]) + [(f"{r}x{r}/Conv1/noise_strength", a())]
+        syn += layer(f"{r}x{r}/ToRGB", ch[r], 3, k=1)
+    for k in range(2 * int(np.log2(R)) - 3):
+        r = 2 ** ((k + 5) // 2)
+        syn.append((f"noise{k}", a(1, 1, r, r)))
+    return {"": [("dlatent_avg", a(wd))], "mapping": mapping, "synthesis": syn}, kw
+
+
+def gen_tf_legacy():
+    """The REFERENCE's legacy.convert_tf_generator (legacy.py:110-204) on tf_generator_tree(), with the oracle
+    Generator standing in for the absent training.networks (as RefG does for the synthesis fixtures): the TF
+    variables in, the converted G's every parameter and buffer out as shape + sha256 of its float32 bytes (bit-exact
+    target of stylemc_amd.legacy), and the converted generator's image on fixed latents."""
+    import json
+    from oracle import networks as ON
+
+    class StandInGenerator(ON.Generator):
+        def __init__(self, z_dim, c_dim, w_dim, img_resolution, img_channels, mapping_kwargs=None,
+                     synthesis_kwargs=None):
+            mk = dict(mapping_kwargs or {})
+            assert mk.pop("embed_features") is None and mk.pop("layer_features") is None
+            assert mk.pop("activation") == "lrelu"
+            super().__init__(z_dim, c_dim, w_dim, img_resolution, img_channels, mapping_kwargs=mk,
+                             **dict(synthesis_kwargs or {}))
+
+    tr = _stub("training")
+    tr.networks = _stub("training.networks", Generator=StandInGenerator)
+    import legacy as ref_legacy                                 # legacy.py
+    tree, kw = tf_generator_tree()
+
+    def net(comp):
+        n = ref_legacy._TFNetworkStub()
+        n.version, n.name, n.static_kwargs = 4, comp or "G", dict(kw) if comp == "" else {}
+        n.variables = list(tree[comp])
+        n.components = {}
+        return n
+
+    tf_G = net("")
+    tf_G.components = {"mapping": net("mapping"), "synthesis": net("synthesis")}
+    G = ref_legacy.convert_tf_generator(tf_G)
+    out = {"static_kwargs": np.array(json.dumps(kw))}
+    for comp, vs in tree.items():
+        out[f"tf_names:{comp}"] = np.array([n for n, _ in vs])
+        for n, v in vs:
+            out[f"tf:{comp}:{n}"] = v
+    import hashlib
+    for n, t in list(G.named_parameters()) + list(G.named_buffers()):   # bit-exact target: shape + sha256 of the bytes
+        a = np.ascontiguousarray(t.detach().numpy().astype(np.float32))
+        out[f"sd:{n}"] = np.array([hashlib.sha256(a.tobytes()).hexdigest()] + [str(d) for d in a.shape])
+    # the converted generator's output on fixed latents (the oracle layers): the GPU test renders the same
+    z = torch.from_numpy(np.random.RandomState(32).standard_normal((2, 32)).astype(np.float32))
+    with torch.no_grad():
+        out["z"] = z
+        out["img"] = G(z, None, truncation_psi=0.7, noise_mode="const")
+    save("tf_legacy.npz", out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     which = sys.argv[1:] or ["upfirdn2d", "bias_act", "conv2d_resample", "synthesis", "irse50", "clip", "nada",
-                             "losses", "styles", "config1", "mapper_train"]
+                             "losses", "styles", "config1", "mapper_train", "tf_legacy"]
     for w in which:
         globals()[f"gen_{w}"]()

@@ -148,3 +148,128 @@ def test_rejects_non_module_reconstructor():
 def test_not_a_network_pickle():
     with pytest.raises(ValueError):
         legacy.load_network_pkl(io.BytesIO(pickle.dumps({"x": 1})))
+
+
+# ------------------------------------------------------------------------------------------- TensorFlow-era pickles
+# tests/golden/tf_legacy.npz: the REFERENCE's legacy.convert_tf_generator (legacy.py:110-204) run on a seeded synthetic
+# TF generator (tests/golden/make_golden.py gen_tf_legacy): its variables, static kwargs, and every converted parameter
+# and buffer.  The TF pickles here are written with the protocol of dnnlib.tflib.network.Network.__getstate__.
+
+
+def _tf_fixture(golden):
+    import json
+    fx = golden("tf_legacy.npz")
+    kw = json.loads(str(fx["static_kwargs"]))
+    comps = {c: [(str(n), fx[f"tf:{c}:{n}"]) for n in fx[f"tf_names:{c}"]] for c in ("", "mapping", "synthesis")}
+    sd = {k[3:]: (str(v[0]), tuple(int(d) for d in v[1:])) for k, v in fx.items() if k.startswith("sd:")}
+    return fx, kw, comps, sd
+
+
+def _same(t, ref):
+    """t (a tensor) equals the fixture entry: shape + sha256 of the float32 bytes."""
+    import hashlib
+    a = np.ascontiguousarray(t.detach().cpu().numpy().astype(np.float32))
+    return a.shape == ref[1] and hashlib.sha256(a.tobytes()).hexdigest() == ref[0]
+
+
+def _fake_tf_module():
+    """`dnnlib.tflib.network.Network` for *writing* TF-era pickles: NEWOBJ + BUILD with the __getstate__ dict."""
+    mod = types.ModuleType("dnnlib.tflib.network")
+
+    class Network:
+        def __init__(self, state):
+            self._state = state
+
+        def __getstate__(self):
+            return self._state
+
+    Network.__module__, Network.__qualname__ = "dnnlib.tflib.network", "Network"
+    mod.Network = Network
+    pkg, sub = types.ModuleType("dnnlib"), types.ModuleType("dnnlib.tflib")
+    pkg.tflib, sub.network = sub, mod
+    return {"dnnlib": pkg, "dnnlib.tflib": sub, "dnnlib.tflib.network": mod}, Network
+
+
+def _tf_pickle(kw, comps, protocol=3):
+    mods, Network = _fake_tf_module()
+    saved = {k: sys.modules.get(k) for k in mods}
+    sys.modules.update(mods)
+    try:
+        def net(name, static, variables, components):
+            return Network(dict(version=4, name=name, static_kwargs=static, components=components,
+                                build_module_src=EVIL_SRC, build_func_name="G_main", variables=variables))
+        G = net("G", dict(kw), comps[""], {"mapping": net("G_mapping", {}, comps["mapping"], {}),
+                                          "synthesis": net("G_synthesis", {}, comps["synthesis"], {})})
+        D = net("D", {}, [("Output/weight", np.zeros((4, 1), np.float32))], {})
+        return pickle.dumps((G, D, G), protocol=protocol)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+
+
+def _stub_tree(kw, comps):
+    def net(static, variables, components):
+        n = legacy.TFNetworkStub()
+        n.__setstate__(dict(version=4, static_kwargs=static, variables=variables, components=components))
+        return n
+    return net(kw, comps[""], {"mapping": net({}, comps["mapping"], {}), "synthesis": net({}, comps["synthesis"], {})})
+
+
+def test_convert_tf_generator_matches_reference(golden):
+    """Every parameter and buffer of the converted generator equals the reference's conversion bit for bit (the
+    Conv0_up flip, transposes, mod_bias + 1, noise indices)."""
+    _, kw, comps, sd_ref = _tf_fixture(golden)
+    conv = legacy.convert_tf_generator(_stub_tree(kw, comps))
+    G = legacy.generator_from_tf(conv, device="cpu")
+    got = dict(list(G.named_parameters()) + list(G.named_buffers()))
+    assert got.keys() == sd_ref.keys()
+    for k, v in sd_ref.items():
+        assert _same(got[k], v), k
+    assert G.img_resolution == 32 and G.synthesis.b32.conv1.weight.shape == (16, 16, 3, 3)
+
+
+@pytest.mark.parametrize("protocol", [2, 3, 4])
+def test_tf_pickle_load(golden, tmp_path, protocol):
+    """A (G, D, Gs) TF-era pickle through the exec-free unpickler (legacy.py:24-30): G_ema converted, the stored
+    build_module_src (raises if executed) never run; the CLI loader path renders from it."""
+    from stylemc_amd.find_direction import load_generator
+    _, kw, comps, sd_ref = _tf_fixture(golden)
+    path = tmp_path / "tf.pkl"
+    path.write_bytes(_tf_pickle(kw, comps, protocol))
+    data = legacy.load_network_pkl(open(path, "rb"))
+    assert isinstance(data["G_ema"], legacy.TFGenerator) and isinstance(data["D"], legacy.TFNetworkStub)
+    assert data["training_set_kwargs"] is None and data["augment_pipe"] is None
+    G = load_generator(str(path), 32, "cpu")
+    for k, v in G.state_dict().items():
+        assert _same(v, sd_ref[k]), k
+
+
+def test_tf_converted_generator_oracle_image(golden):
+    """The converted weights drive the oracle generator to the reference-converted generator's image (the fixture
+    was rendered by the oracle layers on the reference's conversion)."""
+    from oracle import networks as ON
+    fx, kw, comps, _ = _tf_fixture(golden)
+    conv = legacy.convert_tf_generator(_stub_tree(kw, comps))
+    ik = dict(conv.init_kwargs)
+    mk = ik.pop("mapping_kwargs")
+    Go = ON.Generator(**{k: ik.pop(k) for k in ("z_dim", "c_dim", "w_dim", "img_resolution", "img_channels")},
+                      mapping_kwargs=mk, **ik).eval()
+    Go.load_state_dict(conv.state_dict, strict=False)
+    with torch.no_grad():
+        img = Go(torch.from_numpy(fx["z"]), None, truncation_psi=0.7, noise_mode="const")
+    assert torch.equal(img, torch.from_numpy(fx["img"]))
+
+
+def test_tf_kwargs_rejections():
+    with pytest.raises(ValueError, match="Unknown TensorFlow kwarg"):
+        legacy._tf_kwargs({"resolution": 32, "not_a_kwarg": 1})
+    kw = legacy._tf_kwargs({"label_size": 10})
+    with pytest.raises(NotImplementedError):
+        legacy.tf_generator_kwargs(kw)
+    stub = legacy.TFNetworkStub()
+    stub.__setstate__(dict(version=3, static_kwargs={}, variables=[], components={}))
+    with pytest.raises(ValueError, match="version too low"):
+        legacy.convert_tf_generator(stub)
