@@ -25,24 +25,25 @@ RES = 256
 
 
 def problem(dev):
-    from stylemc_amd import networks, synthetic
+    from stylemc_amd import networks, synthetic, utils
     from stylemc_amd.clip_loss import CLIPLoss
     from stylemc_amd.id_loss import IDLoss
     cfg = synthetic.generator_config(resolution=RES)
     G = networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=dev)
     text = synthetic.text_direction("a photo of a face of a feminine woman", "a photo of a face of a man")
     clip = [(CLIPLoss(dev, text_features=text, synthetic_weights=True, seed=4), 1.0)]
-    return G, clip, IDLoss(device=dev, weights=None, seed=3)
+    # get_temp_shapes replaces every affine by Identity (utils.py:100-120): once per generator
+    return G, clip, IDLoss(device=dev, weights=None, seed=3), utils.get_temp_shapes(G)
 
 
-def run_cases(world, dev, G, clip, idl):
+def run_cases(world, dev, G, clip, idl, shapes):
     from stylemc_amd import synthetic
     from stylemc_amd.find_direction import DirectionFinder, initial_delta
     out = {}
     for gb, n_items, steps in CASES:
         styles = synthetic.synthetic_styles(n_items, seed=5).to(dev)
         f = DirectionFinder(G, styles, clip, idl, resolution=RES, batch_size=gb, global_batch=gb, n_epochs=4,
-                            seed=1, world=world, init_delta=initial_delta(0, 0.01))
+                            seed=1, world=world, init_delta=initial_delta(0, 0.01), temp_shapes=shapes)
         assert f.prefetch_orig and f.batch_losses and f._side_stream() is not None, "not the pipelined schedule"
         parts, picks = [], []
         for _ in range(steps):

@@ -126,7 +126,7 @@ def test_identical_steps_bit_equal_ffhq1024():
     same generator, S codes, seeds and start point, two steps each (FFHQ-1024, batch 4, the default three-stream
     schedule) give bit-equal gradients and directions -- no order-dependent float atomics on the path (the
     demodulation gradient dd is summed in a fixed order, csrc/modconv_aux.hip dd_plane_kernel)."""
-    from stylemc_amd import build, networks
+    from stylemc_amd import build, networks, utils
     from stylemc_amd.clip_loss import CLIPLoss
     from stylemc_amd.find_direction import DirectionFinder, initial_delta
     from stylemc_amd.id_loss import IDLoss
@@ -137,10 +137,11 @@ def test_identical_steps_bit_equal_ffhq1024():
     G = networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=DEV)
     clip = [(CLIPLoss(DEV, text_features=text, synthetic_weights=True, seed=4), 1.0)]
     idl = IDLoss(device=DEV, weights=None, seed=3)
+    shapes = utils.get_temp_shapes(G)   # (replaces the affines: once per generator)
     runs = []
     for _ in range(2):
         f = DirectionFinder(G, styles, clip, idl, resolution=1024, batch_size=4, n_epochs=2, seed=0,
-                            init_delta=initial_delta(0, 0.01))
+                            init_delta=initial_delta(0, 0.01), temp_shapes=shapes)
         runs.append([f.step()["grad"].clone() for _ in range(2)] + [f.delta.clone()])
     torch.cuda.synchronize()
     for a, b in zip(*runs):
