@@ -456,12 +456,20 @@ class DirectionFinder:
         return g, static_in, out
 
     def step(self):
+        """One iteration: this rank's shard terms (local_step), the all_reduce, the SGD update (apply_step)."""
+        buf = self.local_step()
+        self.world.all_reduce_(buf)
+        return self.apply_step(buf)
+
+    def local_step(self):
+        """This rank's part of an iteration: the batch pick, the shard's sum-form gradient and loss terms in one
+        fused [8*512 + 4] buffer (zeros for an empty shard), the next batch's prefetch."""
         self.it += 1
-        lr_t = cosine_lr(self.lr0, self.it, self.total_iterations)
         if self._next_i is not None:
             i, self._next_i = self._next_i, None
         else:
             i = self.rng.randint(0, self.num_batches)
+        self._cur_i = i
         lo, hi, (a, b) = self._shard(i)
         self.styles_direction.index_copy_(1, self.t_idx, self.delta)
         buf = torch.zeros(self.delta.numel() + 4, device=self.device)
@@ -474,10 +482,14 @@ class DirectionFinder:
                 self._prefetch_next()
         elif pipelined:
             self._pref = None
-        self.world.all_reduce_(buf)
+        return buf
+
+    def apply_step(self, buf):
+        """The SGD update from the reduced buffer (every rank holds the same one after the all_reduce)."""
+        lr_t = cosine_lr(self.lr0, self.it, self.total_iterations)
         grad = buf[:-4].view_as(self.delta)
         self.delta = torch.add(self.delta, grad, alpha=-lr_t)  # == torch.optim.SGD step (find_direction.py:339)
-        self.last = {"it": self.it, "batch": i, "lr": lr_t, "grad": grad, "parts": buf[-4:]}
+        self.last = {"it": self.it, "batch": self._cur_i, "lr": lr_t, "grad": grad, "parts": buf[-4:]}
         return self.last
 
     def log_line(self):

@@ -36,25 +36,60 @@ def problem(dev):
     return G, clip, IDLoss(device=dev, weights=None, seed=3), utils.get_temp_shapes(G)
 
 
-def run_cases(world, dev, G, clip, idl, shapes):
+def _finder(world, dev, G, clip, idl, shapes, gb, n_items):
     from stylemc_amd import synthetic
     from stylemc_amd.find_direction import DirectionFinder, initial_delta
+    styles = synthetic.synthetic_styles(n_items, seed=5).to(dev)
+    f = DirectionFinder(G, styles, clip, idl, resolution=RES, batch_size=gb, global_batch=gb, n_epochs=4,
+                        seed=1, world=world, init_delta=initial_delta(0, 0.01), temp_shapes=shapes)
+    assert f.prefetch_orig and f.batch_losses and f._side_stream() is not None, "not the pipelined schedule"
+    return f
+
+
+def _record(out, gb, f, parts, picks):
+    torch.cuda.synchronize()
+    out[f"delta_{gb}"] = f.delta.cpu().numpy()
+    out[f"sdir_{gb}"] = f.styles_direction.cpu().numpy()
+    out[f"parts_{gb}"] = torch.stack(parts).numpy()
+    out[f"picks_{gb}"] = np.array(picks)
+
+
+def run_cases(world, dev, G, clip, idl, shapes):
+    """Every CASES problem through DirectionFinder.step with `world` (the real N-rank run, or one rank)."""
     out = {}
     for gb, n_items, steps in CASES:
-        styles = synthetic.synthetic_styles(n_items, seed=5).to(dev)
-        f = DirectionFinder(G, styles, clip, idl, resolution=RES, batch_size=gb, global_batch=gb, n_epochs=4,
-                            seed=1, world=world, init_delta=initial_delta(0, 0.01), temp_shapes=shapes)
-        assert f.prefetch_orig and f.batch_losses and f._side_stream() is not None, "not the pipelined schedule"
+        f = _finder(world, dev, G, clip, idl, shapes, gb, n_items)
         parts, picks = [], []
         for _ in range(steps):
             last = f.step()
             parts.append(last["parts"].cpu())
             picks.append(last["batch"])
-        torch.cuda.synchronize()
-        out[f"delta_{gb}"] = f.delta.cpu().numpy()
-        out[f"sdir_{gb}"] = f.styles_direction.cpu().numpy()
-        out[f"parts_{gb}"] = torch.stack(parts).numpy()
-        out[f"picks_{gb}"] = np.array(picks)
+        _record(out, gb, f, parts, picks)
+    return out
+
+
+def run_cases_simulated(dev, G, clip, idl, shapes, world_size=2):
+    """The N-rank run replayed in ONE process: a finder per rank view (World(rank=r, world_size=N)), in lockstep --
+    each computes its shard's buffer (local_step), the buffers are summed (what all_reduce(SUM) of N = 2 computes,
+    one fp32 add per element), every view applies the sum (apply_step).  Same kernels on the same shard sizes as the
+    real ranks, so the real run must match it bit for bit."""
+    from stylemc_amd import dist as sdist
+    out = {}
+    for gb, n_items, steps in CASES:
+        fs = [_finder(sdist.World(r, world_size, 0, None, 0), dev, G, clip, idl, shapes, gb, n_items)
+              for r in range(world_size)]
+        parts, picks = [], []
+        for _ in range(steps):
+            bufs = [f.local_step() for f in fs]
+            tot = bufs[0]
+            for b in bufs[1:]:
+                tot = tot + b
+            lasts = [f.apply_step(tot.clone()) for f in fs]
+            parts.append(lasts[0]["parts"].cpu())
+            picks.append(lasts[0]["batch"])
+        for f in fs[1:]:
+            assert torch.equal(f.delta, fs[0].delta)
+        _record(out, gb, fs[0], parts, picks)
     return out
 
 

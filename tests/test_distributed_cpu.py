@@ -18,14 +18,18 @@ from stylemc_amd.find_direction import DirectionFinder, initial_delta
 from tests.fd_helpers import OracleCLIP, OracleID, TinyFace, oracle_generator, oracle_rows_synth, tiny_clip_visual
 
 
-def _finder(world, global_batch, n_items=5, steps=3):
+def _make(world, global_batch, n_items=5):
     torch.manual_seed(0)
     G = oracle_generator(16, 256)
     styles = synthetic.synthetic_styles(n_items, seed=1)
     clip = OracleCLIP(tiny_clip_visual(), synthetic.text_direction("a", "b", dim=32))
-    f = DirectionFinder(G, styles, [(clip, 1.0)], OracleID(TinyFace()), resolution=16, batch_size=global_batch,
-                        global_batch=global_batch, learning_rate=1.5, n_epochs=2, seed=3, world=world,
-                        init_delta=initial_delta(0, 0.01), synth_fn=oracle_rows_synth)
+    return DirectionFinder(G, styles, [(clip, 1.0)], OracleID(TinyFace()), resolution=16, batch_size=global_batch,
+                           global_batch=global_batch, learning_rate=1.5, n_epochs=2, seed=3, world=world,
+                           init_delta=initial_delta(0, 0.01), synth_fn=oracle_rows_synth)
+
+
+def _finder(world, global_batch, n_items=5, steps=3):
+    f = _make(world, global_batch, n_items)
     losses = []
     for _ in range(steps):
         last = f.step()
@@ -69,6 +73,32 @@ def test_two_rank_matches_single_rank(tmp_path, global_batch):
     for key, ref in (("delta", ref_delta), ("losses", ref_losses), ("sdir", ref_sdir)):
         err = (got[key] - ref).abs().max().item()
         assert err <= 1e-4 * ref.abs().max().item() + 1e-7, (key, err)
+
+
+def _simulated(global_batch, steps=3):
+    """The 2-rank run replayed in one process: two rank views in lockstep, local_step each, buffers summed (what
+    all_reduce(SUM) of two ranks computes), apply_step each."""
+    fs = [_make(sdist.World(r, 2, 0, None), global_batch) for r in range(2)]
+    losses = []
+    for _ in range(steps):
+        b0, b1 = (f.local_step() for f in fs)
+        tot = b0 + b1
+        lasts = [f.apply_step(tot.clone()) for f in fs]
+        losses.append(lasts[0]["parts"].clone())
+    assert torch.equal(fs[0].delta, fs[1].delta)
+    return fs[0].delta.clone(), torch.stack(losses), fs[0].styles_direction.clone()
+
+
+@pytest.mark.parametrize("global_batch", [4, 3, 1])
+def test_two_rank_matches_lockstep_replay_exactly(tmp_path, global_batch):
+    """The multi-process exchange adds nothing beyond the sum of the shard buffers: bit-equal to the replay."""
+    torch.set_num_threads(1)
+    ref = _simulated(global_batch)
+    out = str(tmp_path / "r0.pt")
+    mp.spawn(_worker, args=(2, _free_port(), global_batch, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    for key, r in zip(("delta", "losses", "sdir"), ref):
+        assert torch.equal(got[key], r), key
 
 
 def test_shard_rows_partition():
