@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 2
+#define SMC_ABI_VERSION 3
 
 #define SMC_OK 0
 #define SMC_ERR_INVALID 1     /* bad argument / shape (reference: TORCH_CHECK -> RuntimeError)   */
@@ -92,7 +92,18 @@ typedef struct {
     const float* wk;      /* [ntaps][cin][cout] packed weights                */
     const float* wino_u;  /* optional (IR-SE50 executor): Winograd F(2x2) taps of a 9-tap 3x3 stride-1 'same'
                              phase from smc_wino_taps_f32, used for its <= 16x16 planes; NULL = none        */
+    const void* wk_x3;    /* optional: wk split into three bf16 terms (smc_conv_weights_x3).  When every phase of a
+                             call has them, the LDS-DMA GEMM runs the fp32 products as split-bf16 MFMAs (each
+                             operand a = a0 + a1 + a2 exactly, the six products a_i b_j with i + j <= 2: error per
+                             product <= 2^-23 |a b|, fp32-class) at 6/16 of the fp32 MFMA's cost; the per-sample
+                             weights of a style-scaled call are split on the fly.  NULL = exact-fp32 MFMA        */
 } smc_conv_phase;
+
+/* Bytes of the split-bf16 planes of a phase's [ntaps][cin][cout] weights (cin % 16 == 0; 0 = unsupported), and
+ * the planes themselves: layout [ntaps][cin/16][3 terms][2 octets][cout][8] bf16, term s of wk[t][16c + 8q + e][o]
+ * at ((((t*(cin/16) + c)*3 + s)*2 + q)*cout + o)*8 + e; wk_x3 16-B aligned. */
+int64_t smc_conv_weights_x3_bytes(int ntaps, int cin, int cout);
+int smc_conv_weights_x3(const float* wk, int ntaps, int cin, int cout, void* wk_x3, void* stream);
 
 #define SMC_EPI_STORE 0   /* y = acc                                                           */
 #define SMC_EPI_MODACT 1  /* u = acc; y = clamp(act(u*d[n,o] + noise*strength + bias[o])*gain)  */

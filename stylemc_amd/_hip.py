@@ -23,7 +23,7 @@ EPI_STORE, EPI_MODACT, EPI_PRELU, EPI_PRELU_GRAD, EPI_AFFINE = 0, 1, 2, 3, 4
 class ConvPhase(ctypes.Structure):
     _fields_ = [("ntaps", c_int), ("tap_dy", c_int * 9), ("tap_dx", c_int * 9), ("in_stride", c_int),
                 ("out_h", c_int), ("out_w", c_int), ("out_oy", c_int), ("out_ox", c_int), ("out_sy", c_int),
-                ("out_sx", c_int), ("wk", c_void_p), ("wino_u", c_void_p)]
+                ("out_sx", c_int), ("wk", c_void_p), ("wino_u", c_void_p), ("wk_x3", c_void_p)]
 
 
 class ConvEpilogue(ctypes.Structure):
@@ -56,6 +56,8 @@ _SIGS = {
     "smc_conv_gemm_workspace_size": (c_int64, [c_int, c_int, c_int, c_int, c_int, P, c_int]),
     "smc_conv_gemm_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, c_int64,
                                   P]),
+    "smc_conv_weights_x3_bytes": (c_int64, [c_int, c_int, c_int]),
+    "smc_conv_weights_x3": (c_int, [P, c_int, c_int, c_int, P, P]),
     "smc_conv3x3_wino_supported": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "smc_conv3x3_wino_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P]),
     "smc_conv3x3_wino_workspace_size": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
@@ -130,7 +132,7 @@ def load(path=None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.smc_abi_version() != 2:
+        if lib.smc_abi_version() != 3:
             raise RuntimeError("stylemc_amd: ABI version mismatch, rebuild the library")
         if path is None:
             _lib = lib

@@ -37,6 +37,8 @@ struct PhaseDev {
     int out_h, out_w, out_oy, out_ox, out_sy, out_sx;
     const float* wk;
     int64_t wstride;  // LDS-DMA kernel: floats between two samples' weights (0 = shared weights)
+    const short* wx3;    // split-bf16 kernel: the three-term bf16 planes of wk (x3_weights_kernel layout)
+    int64_t wx3_stride;  // bf16 elements between two samples' planes (0 = shared weights)
 };
 
 struct GemmParams {
@@ -589,6 +591,243 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_lds_kernel(GemmParams p) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragment reads of this slot done before the next barrier
     }
     gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32, smem);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Split-bf16 form of conv_gemm_lds_kernel: the same tiles, K steps, DMA ring and epilogue, the fp32 products on the
+// bf16 matrix core (v_mfma_f32_32x32x16_bf16) as three-term splits.  Every fp32 operand is split exactly into
+// three bf16 terms, a = a0 + a1 + a2 (truncation: a0 = the top 8 significant bits, a1 the next 8 of a - a0, a2 the
+// last 8), and a * b is accumulated as the six products a_i b_j with i + j <= 2 -- smallest first -- leaving out
+// a1 b2 + a2 b1 + a2 b2 <= 2^-23 |a b|: the error of one fp32 rounding, per product.  The bf16 MFMA runs 16x the
+// fp32 MFMA's FLOP rate, so six of them cost 6/16 of one fp32 product (tools/probes/bx6_probe.hip, LDS-fed tile
+// loop: 146 TF/s fp32 MFMA, 251 TF/s split with the input split in registers; max error vs fp64 9.3e-6 against
+// 1.4e-5 for the fp32 MFMA on the same sums).
+//   * weights (frozen, or the per-sample W * s): split once into planes [taps][cin/16][3][2][cout][8] bf16
+//     (x3_weights_kernel) that the DMA copies as they are: an A fragment (8 consecutive k of one output channel)
+//     is one conflict-free ds_read_b128 per term;
+//   * input: the fp32 slab [BKT][BM] of conv_gemm_lds_kernel; a B fragment (8 consecutive k of one position) is 8
+//     ds_read_b32, split in registers (4 VALU per value + 3 v_perm per pair) and reused by the wave's TO blocks.
+// The C/D layout of the 32x32x16 bf16 MFMA is that of the fp32 32x32x2 one, so gemm_epilogue is shared.
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+// a = t0 + t1 + t2 for each of 8 values, as three bf16x8 fragments (the high halves of a, a - t0, a - t0 - t1)
+__device__ __forceinline__ void x3_split8(const float (&x)[8], bf16x8 (&t)[3]) {
+    unsigned u0[8], u1[8], u2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const unsigned u = __float_as_uint(x[j]);
+        const float r1 = x[j] - __uint_as_float(u & 0xffff0000u);
+        const unsigned v = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(v & 0xffff0000u);
+        u0[j] = u;
+        u1[j] = v;
+        u2[j] = __float_as_uint(r2);
+    }
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 w0, w1, w2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // (high half of element 2j) | (high half of element 2j + 1) << 16
+        w0[j] = __builtin_amdgcn_perm(u0[2 * j + 1], u0[2 * j], 0x07060302u);
+        w1[j] = __builtin_amdgcn_perm(u1[2 * j + 1], u1[2 * j], 0x07060302u);
+        w2[j] = __builtin_amdgcn_perm(u2[2 * j + 1], u2[2 * j], 0x07060302u);
+    }
+    t[0] = __builtin_bit_cast(bf16x8, w0);
+    t[1] = __builtin_bit_cast(bf16x8, w1);
+    t[2] = __builtin_bit_cast(bf16x8, w2);
+}
+
+// acc += a * b over the six split products, smallest first
+__device__ __forceinline__ f32x16 x3_mma(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
+// out[nn][t][ci / 16][s][(ci % 16) / 8][o][ci % 8] = term s of wk[t][ci][o] * (s_in ? s_in[nn][ci] : 1)
+__global__ __launch_bounds__(256) void x3_weights_kernel(const float* wk, const float* s_in, short* out, int ntaps,
+                                                         int cin, int cout, int n) {
+    const int64_t per = (int64_t)ntaps * cin * cout;
+    const int64_t total = per * n;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        // e -> (nn, t, c16, kq, o, ee): ee fastest (the 16-B runs the kernel's DMA reads)
+        const int ee = (int)(e & 7);
+        int64_t r = e >> 3;
+        const int o = (int)(r % cout);
+        r /= cout;
+        const int kq = (int)(r & 1);
+        r >>= 1;
+        const int c16 = (int)(r % (cin / 16));
+        r /= cin / 16;
+        const int t = (int)(r % ntaps);
+        const int nn = (int)(r / ntaps);
+        const int ci = c16 * 16 + kq * 8 + ee;
+        const float v = wk[((int64_t)t * cin + ci) * cout + o] * (s_in ? s_in[(int64_t)nn * cin + ci] : 1.f);
+        const unsigned u = __float_as_uint(v);
+        const float r1 = v - __uint_as_float(u & 0xffff0000u);
+        const unsigned w = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(w & 0xffff0000u);
+        const unsigned term[3] = {u >> 16, w >> 16, __float_as_uint(r2) >> 16};
+        short* dst = out + nn * per * 3;
+#pragma unroll
+        for (int sidx = 0; sidx < 3; ++sidx)
+            dst[((((int64_t)t * (cin / 16) + c16) * 3 + sidx) * 2 + kq) * ((int64_t)cout * 8) + (int64_t)o * 8 + ee] =
+                (short)term[sidx];
+    }
+}
+
+template <int WO, int WM, int TO, int TM, int BKT, int TAG = 0>
+__global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
+    static_assert(WO * WM == 4, "4 waves");
+    static_assert(BKT % 16 == 0, "16-channel chunks");
+    constexpr int BO = WO * TO * 32;
+    constexpr int BM = WM * TM * 32;
+    constexpr int NKC = BKT / 16;                // 16-channel chunks per K step (one bf16 MFMA K each)
+    constexpr int WB = NKC * 6 * BO * 16;         // bytes of the step's weight planes [NKC][3][2][BO][8] bf16
+    constexpr int XB = BKT * BM * 4;              // bytes of the step's input slab [BKT][BM] fp32
+    constexpr int STAGE = WB + XB;
+    constexpr int NCH = BM / 64;                 // 64-position chunks per input row
+    static_assert(NCH >= 1 && NCH <= 4 && 4 % NCH == 0, "BM in {64,128,256}");
+    constexpr int RSTEP = 4 / NCH;
+    constexpr int XI = BKT * NCH / 4;            // input DMAs per wave per step
+    static_assert(WB % 1024 == 0, "weight planes split into whole 1-KB DMAs");
+    constexpr int WLI = WB / 1024;               // weight DMAs per step (whole workgroup)
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wo = wave / WM, wm = wave % WM;
+    const int phase = blockIdx.z / p.nsplit;
+    const int split = blockIdx.z - phase * p.nsplit;
+    const PhaseDev& ph = p.ph[phase];
+    const int hw_out = ph.out_h * ph.out_w;
+    int tm = blockIdx.x, tn = blockIdx.y;
+    if (p.ntn) {  // XCD-aware bijective tile order (conv_gemm_lds_kernel)
+        const int nwg = gridDim.x, orig = blockIdx.x;
+        const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+        const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+        tm = wgid / p.ntn;
+        tn = wgid - tm * p.ntn;
+    }
+    int M = p.n * hw_out;
+    int m0 = tm * BM;
+    if (p.per_sample) {
+        const int tps = (hw_out + BM - 1) / BM;
+        const int nb = tm / tps;
+        if (nb >= p.n) return;
+        m0 = nb * hw_out + (tm - nb * tps) * BM;
+        M = (nb + 1) * hw_out;
+    }
+    if (m0 >= M) return;
+    const int o0 = tn * BO;
+    const int cpk = p.cin / BKT;
+    const int ks_total = ph.ntaps * cpk;
+    const int ks_begin = (int)((int64_t)ks_total * split / p.nsplit);
+    const int ks_end = (int)((int64_t)ks_total * (split + 1) / p.nsplit);
+
+    const int cw = wave % NCH, r0 = wave / NCH;
+    const int m = m0 + cw * 64 + lane;
+    const bool mvalid = m < M;
+    int nn = 0, a = 0, b = 0;
+    if (mvalid) {
+        nn = m / hw_out;
+        const int rem = m - nn * hw_out;
+        a = rem / ph.out_w;
+        b = rem - a * ph.out_w;
+    }
+    const int in_hw = p.in_h * p.in_w;
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * in_hw * 4), 0x00020000);
+    const int xvbase = nn * p.cin * in_hw * 4;
+    const int ay = a * ph.in_stride, bx = b * ph.in_stride;
+    const short* wx = ph.wx3 + (ph.wx3_stride ? (int64_t)(m0 / hw_out) * ph.wx3_stride : 0);
+    const int c16n = p.cin / 16;
+
+    auto issue = [&](int ks, int slot) {
+        const int t = ks / cpk;
+        const int ci0 = (ks - t * cpk) * BKT;
+        const int iy = ay + ph.dy[t], ix = bx + ph.dx[t];
+        const bool ok = mvalid && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w;
+        const int voff = ok ? xvbase + (iy * p.in_w + ix) * 4 : 0x7ffffff0;
+        char* st = smem + slot * STAGE;
+        float* xs = reinterpret_cast<float*>(st + WB);
+#pragma unroll
+        for (int j = 0; j < XI; ++j) {
+            const int row = r0 + RSTEP * j;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                xrsrc, (__attribute__((address_space(3))) void*)(xs + row * BM + cw * 64), 4, voff,
+                (ci0 + row) * in_hw * 4, 0, 0);
+        }
+        // weight planes: 16-B lanes over [NKC][6 = term x octet][BO] (each (term, octet) run of BO lanes contiguous
+        // in global memory at (((t * cin / 16 + chunk) * 6 + run) * cout + o0 + o) * 8 bf16)
+        const int64_t wbase = ((int64_t)t * c16n + ci0 / 16) * 6;
+        for (int j = wave; j < WLI; j += 4) {
+            const int L = j * 64 + lane;
+            const int run = L / BO, o = L - run * BO;   // run = chunk * 6 + term * 2 + octet
+            const short* src = wx + ((wbase + run) * p.cout + o0 + o) * 8;
+            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(st + j * 1024),
+                                             16, 0, 0);
+        }
+    };
+
+    f32x16 acc[TO][TM];
+#pragma unroll
+    for (int i = 0; i < TO; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int kh = lane >> 5, l32 = lane & 31;
+    int issued = ks_begin;
+    if (issued < ks_end) {
+        issue(issued, 0);
+        ++issued;
+    }
+    for (int ks = ks_begin; ks < ks_end; ++ks) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's DMAs for step ks have landed; the other slot is free
+        asm volatile("" ::: "memory");
+        const int slot = (ks - ks_begin) & 1;
+        const char* st = smem + slot * STAGE;
+        const short* Wp = reinterpret_cast<const short*>(st);
+        const float* Xs = reinterpret_cast<const float*>(st + WB);
+        const float* xcol = Xs + wm * TM * 32 + l32;
+#pragma unroll
+        for (int kc = 0; kc < NKC; ++kc) {
+            bf16x8 bt[TM][3], at[TO][3];
+#pragma unroll
+            for (int j = 0; j < TM; ++j) {
+                float xv[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) xv[e] = xcol[(kc * 16 + 8 * kh + e) * BM + j * 32];
+                x3_split8(xv, bt[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < TO; ++i)
+#pragma unroll
+                for (int s = 0; s < 3; ++s)
+                    at[i][s] = *reinterpret_cast<const bf16x8*>(
+                        Wp + ((((kc * 3 + s) * 2 + kh) * BO) + wo * TO * 32 + i * 32 + l32) * 8);
+            __builtin_amdgcn_sched_barrier(0);
+            if (kc == 0 && issued < ks_end) {  // the next step's DMAs under this step's MFMAs
+                issue(issued, (issued - ks_begin) & 1);
+                ++issued;
+            }
+#pragma unroll
+            for (int i = 0; i < TO; ++i)
+#pragma unroll
+                for (int j = 0; j < TM; ++j) acc[i][j] = x3_mma(at[i], bt[j], acc[i][j]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragment reads of this slot done before the next barrier
+    }
+    gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32,
+                                  reinterpret_cast<float*>(smem));
 }
 
 // Row-halo variant for the 3x3 stride-1 'same' convs whose position tiles are row segments (W % BM == 0: the
@@ -1337,10 +1576,18 @@ bool row_ok(int n, int cin, int cout, int in_h, int in_w, int y_h, int y_w, cons
     return seen == 511 && (int64_t)n * cin * in_h * in_w * 4 < (1LL << 31);
 }
 
-// floats of per-sample weights (n x sum_p taps_p * cin * cout), 64-float aligned
+// floats of per-sample weights (n x sum_p taps_p * cin * cout), 64-float aligned; split-bf16 planes (three bf16
+// terms per weight) take 1.5x that
+bool phases_x3(const smc_conv_phase* ph, int nph) {
+    for (int i = 0; i < nph; ++i)
+        if (!ph[i].wk_x3) return false;
+    return nph > 0;
+}
+
 int64_t wsample_floats(int n, int cin, int cout, const smc_conv_phase* ph, int nph) {
     int64_t t = 0;
     for (int i = 0; i < nph; ++i) t += (int64_t)ph[i].ntaps * cin * cout;
+    if (phases_x3(ph, nph)) t = (t * 3 + 1) / 2;
     return ((t * n + 63) / 64) * 64;
 }
 
@@ -1472,6 +1719,7 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     ConvTParams ctp{};
     ConvTTaps ctt{};
     ConvTL tl{};
+    const bool x3 = phases_x3(phases, nphases);  // split-bf16 products (the caller passed wk_x3 planes)
     const bool convt_lds = convt_lds_plan(n, cin, cout, in_h, in_w, y_h, y_w, phases, nphases, epi, &ctt, &tl);
     const bool fused_t = !convt_lds && convt_fusable(cin, cout, in_h, in_w, y_h, y_w, phases, nphases, epi, &ctp);
     const int64_t pre_fl = prescale_floats(n, cin, cout, phases, nphases);
@@ -1521,6 +1769,8 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         d.in_stride = q.in_stride; d.out_h = q.out_h; d.out_w = q.out_w;
         d.out_oy = q.out_oy; d.out_ox = q.out_ox; d.out_sy = q.out_sy; d.out_sx = q.out_sx;
         d.wk = q.wk;
+        d.wx3 = reinterpret_cast<const short*>(q.wk_x3);
+        d.wx3_stride = 0;
         const int64_t M = (int64_t)n * q.out_h * q.out_w;
         if (M > max_m) max_m = M;
     }
@@ -1550,6 +1800,19 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         SMC_CHECK(workspace && workspace_bytes >= need, "smc_conv_gemm_f32: workspace %lld < %lld bytes",
                   (long long)workspace_bytes, (long long)need);
         float* wsamp = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + part);
+        if (x3) {  // the per-sample weights W * s as split-bf16 planes, [phase][n][planes of one sample]
+            short* wp = reinterpret_cast<short*>(wsamp);
+            int64_t off = 0;
+            for (int i = 0; i < nphases; ++i) {
+                const int64_t per = (int64_t)phases[i].ntaps * cin * cout;
+                hipLaunchKernelGGL(x3_weights_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(per * n, 256), 4096)),
+                                   dim3(256), 0, st, phases[i].wk, s_in, wp + off, phases[i].ntaps, cin, cout, n);
+                p.ph[i].wx3 = wp + off;
+                p.ph[i].wx3_stride = per * 3;
+                off += per * 3 * n;
+            }
+            return smc::check_launch("smc_conv_gemm_f32 (per-sample split weights)");
+        }
         int64_t off = 0;
         for (int i = 0; i < nphases; ++i) {
             const int rows = phases[i].ntaps * cin;
@@ -1618,6 +1881,22 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         grid.x *= grid.y;
         grid.y = 1;
         RowTaps rt{};
+        if (x3) {
+            const bool k32 = cfg == 0 && lds_bk32(cfg, cin);
+            if (cfg == 0 && k32 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32, 1>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 0 && k32) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 0 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 16, 1>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 0) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 16>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 3 && cin % 32 == 0 && tag)
+                hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 32, 1>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 3 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 16, 1>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 3) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 16>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 4) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 1, 1, 16>), grid, dim3(NT), 0, st, p);
+            else hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 2, 16>), grid, dim3(NT), 0, st, p);
+            rc = smc::check_launch("smc_conv_gemm_f32 (split-bf16)");
+            if (rc != SMC_OK || nsplit == 1) return rc;
+            return smc_modconv_epilogue_f32(workspace, nsplit, plane_elems, y, n, cout, y_h, y_w, &e, stream);
+        }
         if (nsplit == 1 && !p.per_sample && (cfg == 4 || cfg == 5) &&
             row_ok(n, cin, cout, in_h, in_w, y_h, y_w, phases, nphases, Cfg{c.bo, 256}, &rt)) {
             p.ntn = cout / c.bo;  // column tiles (a 96-channel data gradient: 3 x 32)
@@ -1678,6 +1957,22 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
 }
 
 }  // namespace
+
+SMC_API int64_t smc_conv_weights_x3_bytes(int ntaps, int cin, int cout) {
+    if (ntaps < 1 || ntaps > 9 || cin < 16 || cin % 16 || cout < 1) return 0;
+    return (int64_t)ntaps * cin * cout * 3 * (int64_t)sizeof(short);
+}
+
+SMC_API int smc_conv_weights_x3(const float* wk, int ntaps, int cin, int cout, void* wk_x3, void* stream) {
+    SMC_CHECK(wk && wk_x3, "smc_conv_weights_x3: null pointer");
+    SMC_CHECK(smc_conv_weights_x3_bytes(ntaps, cin, cout) > 0, "smc_conv_weights_x3: bad shape taps=%d cin=%d cout=%d",
+              ntaps, cin, cout);
+    SMC_CHECK((reinterpret_cast<uintptr_t>(wk_x3) & 15) == 0, "smc_conv_weights_x3: planes must be 16-B aligned");
+    const int64_t total = (int64_t)ntaps * cin * cout;
+    hipLaunchKernelGGL(x3_weights_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(total, 256), 4096)), dim3(256),
+                       0, smc::as_stream(stream), wk, nullptr, reinterpret_cast<short*>(wk_x3), ntaps, cin, cout, 1);
+    return smc::check_launch("smc_conv_weights_x3");
+}
 
 SMC_API int smc_conv_gemm_f32(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h,
                               int y_w, const smc_conv_phase* phases, int nphases, const float* s_in,

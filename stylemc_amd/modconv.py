@@ -24,7 +24,7 @@ import torch
 from . import _hip
 
 
-def _phase(taps, in_stride, out_h, out_w, out_oy, out_ox, out_sy, out_sx, wk):
+def _phase(taps, in_stride, out_h, out_w, out_oy, out_ox, out_sy, out_sx, wk, wk_x3=None):
     ph = _hip.ConvPhase()
     ph.ntaps = len(taps)
     for t, (dy, dx) in enumerate(taps):
@@ -33,7 +33,28 @@ def _phase(taps, in_stride, out_h, out_w, out_oy, out_ox, out_sy, out_sx, wk):
     ph.in_stride = in_stride
     ph.out_h, ph.out_w, ph.out_oy, ph.out_ox, ph.out_sy, ph.out_sx = out_h, out_w, out_oy, out_ox, out_sy, out_sx
     ph.wk = wk.data_ptr()
+    ph.wk_x3 = _hip.ptr(wk_x3)
     return ph
+
+
+# Split-bf16 products for the direct implicit-GEMM convs (include/stylemc_hip.h smc_conv_phase.wk_x3): every fp32
+# operand split exactly into three bf16 terms, the six products above 2^-23 |a b| on the bf16 matrix core.  Module
+# switch (tests / tools compare it against the exact-fp32 MFMA kernels).
+X3 = True
+
+
+def x3_planes(wk, cin, cout):
+    """The split-bf16 planes (smc_conv_weights_x3) of [ntaps][cin][cout] GEMM weights, or None where the kernel has
+    no split form (cin % 16) or the weights are not on the GPU."""
+    if not (X3 and wk.is_cuda):
+        return None
+    lib = _hip.load()
+    nb = lib.smc_conv_weights_x3_bytes(wk.shape[0], cin, cout)
+    if nb <= 0:
+        return None
+    out = torch.empty((nb + 15) // 16 * 8, device=wk.device, dtype=torch.int16)
+    _hip.call("smc_conv_weights_x3", wk.data_ptr(), wk.shape[0], cin, cout, out.data_ptr(), _hip.stream())
+    return out
 
 
 class PackedConv:
@@ -63,6 +84,9 @@ class PackedConv:
                     wk = torch.stack([W[:, :, ky, kx].t() for ky, kx in sel]).contiguous()  # [t][i][o]
                     self.phases.append((py, px, [(-(ky - py) // 2, -(kx - px) // 2) for ky, kx in sel], wk))
             self.bwd_taps = [(ky, kx) for ky, kx in taps]  # stride-2 gather over dT
+        # split-bf16 planes of the direct GEMMs' weights (the caller -- LayerSpec -- waits for the packing kernels)
+        self.x3_fwd = x3_planes(self.wk_fwd, self.cin, self.cout) if up == 1 else None
+        self.x3_bwd = x3_planes(self.wk_bwd, self.cout, self.cin)
         self._cache = {}
         self._wino = {}
         self._wino4 = {}
@@ -97,7 +121,7 @@ class PackedConv:
         key = ("f", h, w)
         if key not in self._cache:
             if self.up == 1:
-                arr = (_hip.ConvPhase * 1)(_phase(self.fwd_taps, 1, h, w, 0, 0, 1, 1, self.wk_fwd))
+                arr = (_hip.ConvPhase * 1)(_phase(self.fwd_taps, 1, h, w, 0, 0, 1, 1, self.wk_fwd, self.x3_fwd))
                 self._cache[key] = (arr, 1, h, w)
             else:
                 th, tw = 2 * h + 1, 2 * w + 1
@@ -110,7 +134,8 @@ class PackedConv:
         key = ("b", h, w)
         if key not in self._cache:
             stride = 1 if self.up == 1 else 2
-            self._cache[key] = ((_hip.ConvPhase * 1)(_phase(self.bwd_taps, stride, h, w, 0, 0, 1, 1, self.wk_bwd)), 1)
+            self._cache[key] = ((_hip.ConvPhase * 1)(_phase(self.bwd_taps, stride, h, w, 0, 0, 1, 1, self.wk_bwd,
+                                                            self.x3_bwd)), 1)
         return self._cache[key]
 
 

@@ -37,7 +37,7 @@ def test_exports_are_only_the_abi():
 
 def test_abi_version_and_errors_without_gpu():
     lib = _hip.load()
-    assert lib.smc_abi_version() == 2
+    assert lib.smc_abi_version() == 3
     # argument validation runs on the host: no GPU needed, must fail loudly with a message
     rc = lib.smc_upfirdn2d_f32(None, None, None, 1, 4, 4, 99, 99, 4, 4, 1, 1, 1, 1, 1, 1, 1, 1, 0, 1.0, None)
     assert rc == 1

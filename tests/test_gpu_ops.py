@@ -235,14 +235,23 @@ def test_synthesis_layer_grad_subsets():
     close(dxc, dxa, 1e-6, "dx only")
 
 
+@pytest.fixture(params=[True, False], ids=["x3", "fp32"])
+def x3(request, monkeypatch):
+    """Both product forms of the direct GEMM: split-bf16 (modconv.X3, the default) and the exact-fp32 MFMA."""
+    from stylemc_amd import modconv
+    monkeypatch.setattr(modconv, "X3", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("n,cin,cout,r", [(2, 32, 32, 256), (4, 64, 32, 128), (1, 32, 32, 1024), (2, 64, 64, 128),
                                            (1, 96, 64, 256), (2, 64, 64, 256), (1, 128, 128, 128), (1, 256, 256, 128),
-                                           (2, 512, 512, 16)])
-def test_conv_gemm_same3x3_vs_conv2d(n, cin, cout, r):
+                                           (2, 512, 512, 16), (4, 512, 512, 8), (3, 128, 64, 24)])
+def test_conv_gemm_same3x3_vs_conv2d(n, cin, cout, r, x3):
     """3x3 'same' convs (conv1 forward with per-sample style-scaled weights, and its data gradient with the
     shared flipped weights) against an fp64 CPU convolution (no activation, so no kinks: tolerance 2e-5 of the
-    max).  32 / 64 output channels with W % 256 == 0 run the row-halo kernel (conv_row_kernel, both tile
-    widths); the other shapes the tap-major LDS-DMA kernel."""
+    max).  Exact-fp32 MFMA: 32 / 64 output channels with W % 256 == 0 run the row-halo kernel (conv_row_kernel,
+    both tile widths), the other shapes the tap-major LDS-DMA kernel; split-bf16 (x3): every shape the LDS-DMA
+    tiles with split products (per-sample split weights in the forward, split-K at 8 and 16 px)."""
     import torch.nn.functional as F
     from stylemc_amd import _hip, modconv
     gen = torch.Generator().manual_seed(11)
@@ -261,6 +270,29 @@ def test_conv_gemm_same3x3_vs_conv2d(n, cin, cout, r):
     modconv.gemm(g.to(DEV), dx, phb, nphb, cout, cin, epi=modconv._epilogue(_hip.EPI_STORE))
     refb = F.conv_transpose2d(g.double(), W.double(), padding=1)
     close(dx, refb, 2e-5, "data grad")
+    assert (P.x3_fwd is not None) == x3
+
+
+@pytest.mark.parametrize("n,cin,cout,h", [(2, 64, 32, 64), (1, 32, 32, 128), (2, 512, 512, 4), (3, 256, 128, 16),
+                                           (1, 128, 64, 64)])
+def test_conv_gemm_stride2_gather_vs_conv2d(n, cin, cout, h, x3):
+    """The up = 2 layers' data gradient through the transposed conv: the stride-2 3x3 gather over dT (2h + 1 rows,
+    a padded pitch) against an fp64 conv2d(stride 2) of the same dT -- both product forms (tolerance 2e-5 of the
+    max)."""
+    import torch.nn.functional as F
+    from stylemc_amd import _hip, modconv
+    gen = torch.Generator().manual_seed(17)
+    W = torch.randn(cout, cin, 3, 3, generator=gen)
+    P = modconv.PackedConv(W.to(DEV), 2)
+    th = 2 * h + 1
+    g = torch.randn(n, cout, th, th, generator=gen)
+    phb, nphb = P.bwd_phases(h, h)
+    dx = torch.empty(n, cin, h, h, device=DEV)
+    modconv.gemm(g.to(DEV), dx, phb, nphb, cout, cin, epi=modconv._epilogue(_hip.EPI_STORE))
+    ref = F.conv2d(g.double(), W.transpose(0, 1).double(), stride=2)
+    assert ref.shape == dx.shape, (ref.shape, dx.shape)
+    close(dx, ref, 2e-5, "stride-2 gather")
+    assert (P.x3_bwd is not None) == x3
 
 
 @pytest.mark.parametrize("n,cin,cout,h", [(2, 64, 32, 64), (1, 128, 64, 128), (2, 512, 512, 4), (3, 256, 128, 16),
