@@ -1411,6 +1411,182 @@ __global__ __launch_bounds__(NT, 2) void convt_lds_kernel(GemmParams p, ConvTTap
     }
 }
 
+// Split-bf16 form of convt_lds_kernel (the products as in conv_gemm_x3_kernel): per K step (16 channels, one input
+// shift) the fp32 input slab [16][BM] and, for every phase reading that shift, its weight planes [3][2][BO][8] bf16;
+// a wave splits each B fragment once and feeds it to every phase's A fragments.
+template <int WO, int WM, int TO, int TM>
+__global__ __launch_bounds__(NT, 2) void convt_x3_kernel(GemmParams p, ConvTTaps tt) {
+    static_assert(WO * WM == 4, "4 waves");
+    constexpr int BKT = 16;
+    constexpr int BO = WO * TO * 32;
+    constexpr int BM = WM * TM * 32;
+    constexpr int NCH = BM / 64;
+    static_assert(NCH >= 1 && NCH <= 4 && 4 % NCH == 0, "BM in {64,128,256}");
+    constexpr int RSTEP = 4 / NCH;
+    constexpr int XI = BKT * NCH / 4;
+    constexpr int PB = 6 * BO * 16;              // bytes of one phase's planes per step
+    static_assert(PB % 1024 == 0, "phase planes split into whole 1-KB DMAs");
+    constexpr int XB = BKT * BM * 4;
+    constexpr int STAGE = XB + 4 * PB;           // input slab + up to 4 phases' planes
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wo = wave / WM, wm = wave % WM;
+    const int gh = p.in_h + 1, gw = p.in_w + 1, hw_g = gh * gw;
+    int tm = blockIdx.x, tn = blockIdx.y;
+    if (p.ntn) {
+        const int nwg = gridDim.x, orig = blockIdx.x;
+        const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+        const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+        tm = wgid / p.ntn;
+        tn = wgid - tm * p.ntn;
+    }
+    int M = p.n * hw_g;
+    int m0 = tm * BM;
+    if (p.per_sample) {
+        const int tps = (hw_g + BM - 1) / BM;
+        const int nb = tm / tps;
+        if (nb >= p.n) return;
+        m0 = nb * hw_g + (tm - nb * tps) * BM;
+        M = (nb + 1) * hw_g;
+    }
+    if (m0 >= M) return;
+    const int o0 = tn * BO;
+    const int split = blockIdx.z;
+    const int cpk = p.cin / BKT;
+    const int c_begin = (int)((int64_t)cpk * split / p.nsplit);
+    const int c_end = (int)((int64_t)cpk * (split + 1) / p.nsplit);
+    const int ks_begin = 4 * c_begin, ks_end = 4 * c_end;
+
+    const int cw = wave % NCH, r0 = wave / NCH;
+    const int m = m0 + cw * 64 + lane;
+    const bool mvalid = m < M;
+    int nn = 0, a = 0, b = 0;
+    if (mvalid) {
+        nn = m / hw_g;
+        const int rem = m - nn * hw_g;
+        a = rem / gw;
+        b = rem - a * gw;
+    }
+    const int in_hw = p.in_h * p.in_w;
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * in_hw * 4), 0x00020000);
+    const int xvbase = nn * p.cin * in_hw * 4;
+    const int wn = m0 / hw_g;
+    const int c16n = p.cin / 16;
+
+    auto issue = [&](int ks, int slot) {
+        const int c = ks >> 2, sh = ks & 3;
+        const int ci0 = c * BKT;
+        const int iy = a - (sh & 1), ix = b - (sh >> 1);
+        const bool ok = mvalid && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w;
+        const int voff = ok ? xvbase + (iy * p.in_w + ix) * 4 : 0x7ffffff0;
+        char* st = smem + slot * STAGE;
+        float* xs = reinterpret_cast<float*>(st);
+#pragma unroll
+        for (int j = 0; j < XI; ++j) {
+            const int row = r0 + RSTEP * j;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                xrsrc, (__attribute__((address_space(3))) void*)(xs + row * BM + cw * 64), 4, voff,
+                (ci0 + row) * in_hw * 4, 0, 0);
+        }
+        const int nph = shift_nph(sh);
+        for (int j = wave; j < nph * (PB / 1024); j += 4) {
+            const int pj = j / (PB / 1024);          // which phase of this shift
+            const int phase = sh == 0 ? pj : (sh == 1 ? (pj ? 1 : 0) : (sh == 2 ? (pj ? 2 : 0) : 0));
+            const int L = (j - pj * (PB / 1024)) * 64 + lane;
+            const int run = L / BO, o = L - run * BO;
+            const PhaseDev& q = p.ph[phase];
+            const short* src = q.wx3 + (q.wx3_stride ? (int64_t)wn * q.wx3_stride : 0) +
+                               ((((int64_t)tt.tap[sh][phase] * c16n + ci0 / 16) * 6 + run) * p.cout + o0 + o) * 8;
+            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(st + XB + j * 1024),
+                                             16, 0, 0);
+        }
+    };
+
+    f32x16 acc[4][TO][TM];
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+        for (int i = 0; i < TO; ++i)
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[ph][i][j][r] = 0.f;
+
+    const int kh = lane >> 5, l32 = lane & 31;
+    if (ks_begin < ks_end) issue(ks_begin, 0);
+    auto step = [&](auto S_, int ks) {
+        constexpr int S = decltype(S_)::value;
+        constexpr int NP = shift_nph(S);
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const char* st = smem + (S & 1) * STAGE;
+        const float* xcol = reinterpret_cast<const float*>(st) + wm * TM * 32 + l32;
+        bf16x8 bt[TM][3];
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+            float xv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[e] = xcol[(8 * kh + e) * BM + j * 32];
+            x3_split8(xv, bt[j]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + 1 < ks_end) issue(ks + 1, (S + 1) & 1);
+#pragma unroll
+        for (int pj = 0; pj < NP; ++pj) {
+            const short* Wp = reinterpret_cast<const short*>(st + XB + pj * PB);
+            bf16x8 at[TO][3];
+#pragma unroll
+            for (int i = 0; i < TO; ++i)
+#pragma unroll
+                for (int s = 0; s < 3; ++s)
+                    at[i][s] = *reinterpret_cast<const bf16x8*>(Wp + (((s * 2 + kh) * BO) + wo * TO * 32 + i * 32 + l32) * 8);
+#pragma unroll
+            for (int i = 0; i < TO; ++i)
+#pragma unroll
+                for (int j = 0; j < TM; ++j)
+                    acc[shift_phase<S>(pj)][i][j] = x3_mma(at[i], bt[j], acc[shift_phase<S>(pj)][i][j]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    for (int ks = ks_begin; ks < ks_end; ks += 4) {
+        step(std::integral_constant<int, 0>{}, ks);
+        step(std::integral_constant<int, 1>{}, ks + 1);
+        step(std::integral_constant<int, 2>{}, ks + 2);
+        step(std::integral_constant<int, 3>{}, ks + 3);
+    }
+
+    float* dst = p.nsplit > 1 ? p.y + (int64_t)split * p.split_stride : p.y;
+    const int64_t plane = (int64_t)p.y_h * p.y_w;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+        const int mc = m0 + wm * TM * 32 + j * 32 + l32;
+        if (mc >= M) continue;
+        const int en = mc / hw_g;
+        const int erem = mc - en * hw_g;
+        const int ea = erem / gw;
+        const int eb = erem - ea * gw;
+#pragma unroll
+        for (int i = 0; i < TO; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = o0 + wo * TO * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                float* row0 = dst + ((int64_t)en * p.cout + o) * plane + (int64_t)(2 * ea) * p.y_w + 2 * eb;
+                row0[0] = acc[0][i][j][r];
+                if (eb < p.in_w) row0[1] = acc[1][i][j][r];
+                if (ea < p.in_h) {
+                    row0[p.y_w] = acc[2][i][j][r];
+                    if (eb < p.in_w) row0[p.y_w + 1] = acc[3][i][j][r];
+                }
+            }
+        }
+    }
+}
+
 // Does this 4-phase description match the polyphase stride-2 transposed 3x3 conv built by
 // stylemc_amd.modconv.PackedConv (phase index py*2+px, taps at shifts {0,-1}^2)?  Fills the table.
 bool convt_structure(int cin, int cout, int in_h, int in_w, int y_h, int y_w, const smc_conv_phase* ph, int nph,
@@ -1836,7 +2012,9 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         p.per_sample = t_per_sample ? 1 : 0;
         p.ntn = cout / tl.bo;
         dim3 g((unsigned)(mt * p.ntn), 1, (unsigned)nsplit);
-        if (tl.id == 1) hipLaunchKernelGGL((convt_lds_kernel<2, 2, 1, 2, 16>), g, dim3(NT), 0, st, p, ctt);
+        if (x3 && tl.id == 1) hipLaunchKernelGGL((convt_x3_kernel<2, 2, 1, 2>), g, dim3(NT), 0, st, p, ctt);
+        else if (x3) hipLaunchKernelGGL((convt_x3_kernel<1, 4, 1, 1>), g, dim3(NT), 0, st, p, ctt);
+        else if (tl.id == 1) hipLaunchKernelGGL((convt_lds_kernel<2, 2, 1, 2, 16>), g, dim3(NT), 0, st, p, ctt);
         else hipLaunchKernelGGL((convt_lds_kernel<1, 4, 1, 1, 16>), g, dim3(NT), 0, st, p, ctt);
         rc = smc::check_launch("smc_conv_gemm_f32 (fused transposed conv, LDS-DMA)");
         if (rc != SMC_OK || nsplit == 1) return rc;

@@ -87,6 +87,7 @@ class PackedConv:
         # split-bf16 planes of the direct GEMMs' weights (the caller -- LayerSpec -- waits for the packing kernels)
         self.x3_fwd = x3_planes(self.wk_fwd, self.cin, self.cout) if up == 1 else None
         self.x3_bwd = x3_planes(self.wk_bwd, self.cout, self.cin)
+        self.x3_phases = [x3_planes(wk, self.cin, self.cout) for _, _, _, wk in self.phases] if up == 2 else None
         self._cache = {}
         self._wino = {}
         self._wino4 = {}
@@ -125,8 +126,8 @@ class PackedConv:
                 self._cache[key] = (arr, 1, h, w)
             else:
                 th, tw = 2 * h + 1, 2 * w + 1
-                ph = [_phase(t, 1, (th - py + 1) // 2, (tw - px + 1) // 2, py, px, 2, 2, wk)
-                      for py, px, t, wk in self.phases]
+                ph = [_phase(t, 1, (th - py + 1) // 2, (tw - px + 1) // 2, py, px, 2, 2, wk, wx)
+                      for (py, px, t, wk), wx in zip(self.phases, self.x3_phases)]
                 self._cache[key] = ((_hip.ConvPhase * 4)(*ph), 4, th, tw)
         return self._cache[key]
 

@@ -53,6 +53,14 @@ def _gpu():
     torch.backends.cuda.matmul.allow_tf32 = False
 
 
+@pytest.fixture(params=[True, False], ids=["x3", "fp32"])
+def x3(request, monkeypatch):
+    """Both product forms of the direct GEMM: split-bf16 (modconv.X3, the default) and the exact-fp32 MFMA."""
+    from stylemc_amd import modconv
+    monkeypatch.setattr(modconv, "X3", request.param)
+    return request.param
+
+
 ACTS = ["linear", "relu", "lrelu", "tanh", "sigmoid", "elu", "selu", "softplus", "swish"]
 
 
@@ -235,14 +243,6 @@ def test_synthesis_layer_grad_subsets():
     close(dxc, dxa, 1e-6, "dx only")
 
 
-@pytest.fixture(params=[True, False], ids=["x3", "fp32"])
-def x3(request, monkeypatch):
-    """Both product forms of the direct GEMM: split-bf16 (modconv.X3, the default) and the exact-fp32 MFMA."""
-    from stylemc_amd import modconv
-    monkeypatch.setattr(modconv, "X3", request.param)
-    return request.param
-
-
 @pytest.mark.parametrize("n,cin,cout,r", [(2, 32, 32, 256), (4, 64, 32, 128), (1, 32, 32, 1024), (2, 64, 64, 128),
                                            (1, 96, 64, 256), (2, 64, 64, 256), (1, 128, 128, 128), (1, 256, 256, 128),
                                            (2, 512, 512, 16), (4, 512, 512, 8), (3, 128, 64, 24)])
@@ -297,7 +297,7 @@ def test_conv_gemm_stride2_gather_vs_conv2d(n, cin, cout, h, x3):
 
 @pytest.mark.parametrize("n,cin,cout,h", [(2, 64, 32, 64), (1, 128, 64, 128), (2, 512, 512, 4), (3, 256, 128, 16),
                                            (1, 512, 256, 32), (2, 32, 32, 33), (4, 512, 512, 8)])
-def test_conv_gemm_transposed_vs_conv_transpose2d(n, cin, cout, h):
+def test_conv_gemm_transposed_vs_conv_transpose2d(n, cin, cout, h, x3):
     """The up = 2 layers' stride-2 transposed 3x3 conv (conv2d_resample.py:125-138 before the blur) as the
     phase-fused LDS-DMA kernel: per-sample style-scaled weights with tiles restarted per image ((h+1)^2 not a
     tile multiple), a prescaled input at the low resolutions, split-K over channel chunks; vs fp64
@@ -314,6 +314,7 @@ def test_conv_gemm_transposed_vs_conv_transpose2d(n, cin, cout, h):
     modconv.gemm(x.to(DEV), t, ph, nph, cin, cout, s=s.to(DEV), epi=modconv._epilogue(_hip.EPI_STORE))
     ref = F.conv_transpose2d((x * s[:, :, None, None]).double(), W.transpose(0, 1).double(), stride=2)
     close(t, ref, 2e-5, "transposed conv")
+    assert all((w is not None) == x3 for w in P.x3_phases)
 
 
 def _misaligned(t):
