@@ -16,6 +16,7 @@ from torch import nn
 
 from . import _hip
 from .id_loss.model_irse import Backbone
+from . import modconv
 from .modconv import _phase
 
 P = ctypes.c_void_p
@@ -84,7 +85,12 @@ class _Packed:
             return d(t).data_ptr()
 
         def phase(taps, stride, oh, ow, wk, oy=0, ox=0, sy=1, sx=1):
-            return _phase(taps, stride, oh, ow, oy, ox, sy, sx, d(wk))
+            wk = d(wk)
+            # split-bf16 planes for the direct GEMMs (modconv.X3; kept alive with the packed weights)
+            wx = modconv.x3_planes(wk, wk.shape[1], wk.shape[2])
+            if wx is not None:
+                self.keep.append(wx)
+            return _phase(taps, stride, oh, ow, oy, ox, sy, sx, wk, wx)
 
         def same_adjoint(W, h, w, in_scale=None, out_scale=None):
             k = W.shape[2]
