@@ -168,7 +168,7 @@ class DirectionFinder:
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
                  overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None, G2=None, temp_shapes2=None,
-                 prefetch_id=True, prefetch_clip=False, graph_prefetch=False, prefetch_after="forward"):
+                 prefetch_id=True):
         self.G = G
         # the edited image's generator (train_latent_mapper.py:100-106,159-162 --network2; default G itself)
         self.G_edit = G2 if G2 is not None else G
@@ -184,23 +184,12 @@ class DirectionFinder:
         # (tools/sensitivity.py: dropping it saves 1.8 ms, dropping CLIP nothing), so its critical-path share is
         # cut to the edited images' forward + backward; CLIP keeps the [edited; original] batch
         self.prefetch_id = prefetch_id
-        # ... and its CLIP embeddings (then CLIP too sees only the edited images on the critical path)
-        self.prefetch_clip = prefetch_clip
-        # the prefetch (no-gradient synthesis + its loss features: ~200 launches, fixed shapes) replayed as a
-        # captured HIP graph: one host call instead of the launches' Python + ctypes enqueue, which bounded the
-        # step where the GPU ran ahead of the host (the low-resolution layers, the loss heads).  Two graphs with
-        # their own static outputs, used alternately: a replay never overwrites the image / features the previous
-        # iteration's losses and backward may still read.  Falls back to eager launches if capture fails.
-        # Off: measured slower, 19.36-19.45 against 18.69-18.76 ms / step eager (profiles/r03_graph_prefetch_ab.txt).
-        self.graph_prefetch = graph_prefetch
-        # where the prefetch may start on the GPU: "forward" (after this iteration's edited forward: beside the
-        # latency-bound loss networks and the backward), "losses" (after the loss networks' forward: beside the
-        # backward only) or "none" (as soon as it is enqueued)
-        assert prefetch_after in ("forward", "losses", "none"), prefetch_after
-        self.prefetch_after = prefetch_after
-        self._loss_done = None
-        self._graphs = {}
-        self._graph_flip = 0
+        # Measured and removed (round 4): the original image's CLIP embeddings prefetched too (19.87-20.01 against
+        # 19.58-19.71 ms / step, profiles/r03_clip_prefetch_ab.txt), the prefetch replayed as a captured HIP graph
+        # (0.7 ms / step slower, profiles/r03_graph_prefetch_ab.txt), the prefetch started after the loss networks'
+        # forward or as soon as enqueued instead of after the edited forward (19.46 / 19.05-19.17 against
+        # 18.83-18.87 ms, profiles/r03_prefetch_start_ab.txt).  The prefetch starts after this iteration's edited
+        # forward (the _fwd_done event).
         self._next_i = None
         self._pref = None
         # edited + original image through each loss network as ONE batch (backward for the edited half)
@@ -370,9 +359,6 @@ class DirectionFinder:
     def _finish(self, styles, d, id_terms, clip_terms, denom):
         T = S_TRAINABLE_SPACE_CHANNELS
         sT = styles.index_select(1, self.t_idx)
-        if self.prefetch_after == "losses" and d.is_cuda:
-            self._loss_done = torch.cuda.Event()
-            self._loss_done.record(torch.cuda.current_stream())
         if FUSED_TOTAL:
             total, parts = _LossTotal.apply(id_terms, clip_terms, d, sT, self.coef["id"], self.coef["clip"],
                                             self.coef["l2"], float(denom * len(T) * 512), float(denom))
@@ -405,55 +391,15 @@ class DirectionFinder:
             return
         if getattr(self, "_pre", None) is None:
             self._pre = self.stream_factory(self.device)
-        if self.prefetch_after == "forward":
-            self._pre.wait_event(self._fwd_done)
-        elif self.prefetch_after == "losses" and self._loss_done is not None:
-            self._pre.wait_event(self._loss_done)
+        self._pre.wait_event(self._fwd_done)
         with torch.cuda.stream(self._pre), torch.no_grad():
-            out = self._graph_replay(self.styles_array[a:b]) if self.graph_prefetch else None
-            if out is None:
-                out = self._prefetch_body(self.styles_array[a:b])
+            out = self._prefetch_body(self.styles_array[a:b])
         self._pref = ((a, b),) + out
 
     def _prefetch_body(self, styles):
         orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
         feats = self.id_loss.target_feats(orig) if self.prefetch_id else None
-        embs = ([cl.encode_src(s) for (cl, _), (_, s) in zip(self.clip_losses, self._clip_inputs(None, orig))]
-                if self.prefetch_clip else None)
-        return orig, feats, embs
-
-    def _graph_replay(self, styles):
-        """The prefetch body as a HIP graph replay on the current (prefetch) stream; captured on first use per
-        batch shape, two instances alternating.  None: capture failed (eager from then on)."""
-        key = (tuple(styles.shape), self._graph_flip)
-        self._graph_flip ^= 1
-        ent = self._graphs.get(key)
-        if ent is None:
-            try:
-                ent = self._graph_capture(styles)
-            except Exception as exc:  # a non-capturable op on this path: stay eager
-                warnings.warn(f"find_direction: prefetch graph capture failed ({exc}); eager prefetch")
-                self.graph_prefetch = False
-                return None
-            self._graphs[key] = ent
-        g, static_in, out = ent
-        static_in.copy_(styles)
-        g.replay()
-        return out
-
-    def _graph_capture(self, styles):
-        cur = torch.cuda.current_stream()
-        static_in = styles.clone()
-        cap = torch.cuda.Stream(device=styles.device)
-        cap.wait_stream(cur)
-        with torch.cuda.stream(cap):
-            self._prefetch_body(static_in)   # warm-up: lazily built state (packed weights, workspaces) first
-            cap.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=cap):
-                out = self._prefetch_body(static_in)
-        cur.wait_stream(cap)
-        return g, static_in, out
+        return orig, feats, None
 
     def step(self):
         """One iteration: this rank's shard terms (local_step), the all_reduce, the SGD update (apply_step)."""

@@ -68,9 +68,8 @@ def main():
 
     variants = {"default": (clip, idl, {}), "no_clip": ([(free, 1.0)], idl, {}), "no_irse": (clip, free, {}),
                 "no_losses": ([(free, 1.0)], free, {}), "no_prefetch": (clip, idl, dict(prefetch_orig=False)),
-                "irse_pair": (clip, idl, dict(prefetch_id=False)), "clip_pref": (clip, idl, dict(prefetch_clip=True)),
-                "side_hi": (clip, idl, {}), "graph": (clip, idl, dict(graph_prefetch=True)), "unfused": (clip, idl, {}),
-                "pref_losses": (clip, idl, dict(prefetch_after="losses")), "pref_none": (clip, idl, dict(prefetch_after="none")),
+                "irse_pair": (clip, idl, dict(prefetch_id=False)),
+                "side_hi": (clip, idl, {}), "unfused": (clip, idl, {}),
                 "main_side_hi": (clip, idl, {})}
     name = sys.argv[sys.argv.index("--variant") + 1]
     clips, idloss, kw = variants[name]
