@@ -3,7 +3,9 @@
     python tools/prof_summary.py gpurun_out/prof1/run_kernel_trace.csv --steps N > profiles/rXX_summary.md
 
 Only kernels from the first synthesis GEMM launch on are counted (model construction before it -- weight
-uploads, packing -- is not part of a step); N = the steps run from there (bench warm-up + timed steps).
+uploads, packing -- is not part of a step); N = the steps run from there (bench warm-up + timed + roofline steps).
+Without --steps, N is inferred from the CLIP tower: every find_direction step runs the ViT patch permutation
+twice (im2col in the forward of the [edited; original] batch, its inverse in the backward).
 Reports the top kernels and the aggregate of the synthesis modconv GEMM family (conv_gemm_lds_kernel /
 conv_gemm_kernel / conv_row_kernel / convt_gemm_kernel instantiations with TAG 0 -- the IR-SE50 executor's
 launches of the same kernels carry TAG 1 and are reported separately), whose average launch duration
@@ -40,6 +42,11 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     first = next(i for i, r in enumerate(rows) if is_family(r["Kernel_Name"]))
     rows = rows[first:]
+    how = "given"
+    if steps is None:
+        perm = sum(1 for r in rows if "patch_perm_kernel" in r["Kernel_Name"])
+        if perm >= 2:
+            steps, how = perm // 2, "inferred: ViT patch permutations / 2"
     tot, cnt = defaultdict(float), defaultdict(int)
     for r in rows:
         d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
@@ -49,6 +56,7 @@ def main():
     span = int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])
     per = f" = {total / 1e6 / steps:.2f} ms/step" if steps else ""
     print(f"# rocprofv3 kernel trace: `{path}`\n")
+    print(f"steps in the trace: {steps} ({how})\n" if steps else "steps in the trace: unknown (pass --steps)\n")
     print(f"from the first synthesis GEMM on: {len(rows)} launches, GPU kernel time {total / 1e6:.2f} ms{per} "
           f"(summed over streams), wall span {span / 1e6:.2f} ms" + (f" = {span / 1e6 / steps:.2f} ms/step" if steps else ""))
     fam = {k: v for k, v in tot.items() if is_family(k) and ", 1>(" not in k}
