@@ -33,7 +33,7 @@ def _phase(taps, in_stride, out_h, out_w, out_oy, out_ox, out_sy, out_sx, wk, wk
     ph.in_stride = in_stride
     ph.out_h, ph.out_w, ph.out_oy, ph.out_ox, ph.out_sy, ph.out_sx = out_h, out_w, out_oy, out_ox, out_sy, out_sx
     ph.wk = wk.data_ptr()
-    ph.wk_x3 = _hip.ptr(wk_x3)
+    ph.wk_x3 = wk_x3.data_ptr() if wk_x3 is not None else None
     return ph
 
 
