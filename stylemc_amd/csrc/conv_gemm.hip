@@ -679,7 +679,16 @@ __global__ __launch_bounds__(256) void x3_weights_kernel(const float* wk, const 
     }
 }
 
-template <int WO, int WM, int TO, int TM, int BKT, int TAG = 0>
+// Ring depth of the split-bf16 kernel (A/B knob: SMC_AB_DEFINES=-DSMC_X3_NST=n builds a variant library).  Its K step
+// holds 2.67x fewer MFMA cycles than the fp32 kernel's, so the DMA latency a 2-stage ring leaves exposed is larger.
+#ifndef SMC_X3_NST
+#define SMC_X3_NST 2
+#endif
+#ifndef SMC_X3_K32_SMALL
+#define SMC_X3_K32_SMALL 0
+#endif
+
+template <int WO, int WM, int TO, int TM, int BKT, int TAG = 0, int NST = SMC_X3_NST>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
     static_assert(WO * WM == 4, "4 waves");
     static_assert(BKT % 16 == 0, "16-channel chunks");
@@ -695,7 +704,11 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
     constexpr int XI = BKT * NCH / 4;            // input DMAs per wave per step
     static_assert(WB % 1024 == 0, "weight planes split into whole 1-KB DMAs");
     constexpr int WLI = WB / 1024;               // weight DMAs per step (whole workgroup)
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    constexpr int WIW = (WLI + 3) / 4;           // ... per wave (the last round re-issues early ones: same bytes, same
+                                                 // place), so every wave counts the same DMAs per step
+    constexpr int PER = XI + WIW;
+    static_assert(NST >= 2 && NST <= 4 && PER * (NST - 2) <= 63, "vmcnt range");
+    __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -765,7 +778,10 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
         // weight planes: 16-B lanes over [NKC][6 = term x octet][BO] (each (term, octet) run of BO lanes contiguous
         // in global memory at (((t * cin / 16 + chunk) * 6 + run) * cout + o0 + o) * 8 bf16)
         const int64_t wbase = ((int64_t)t * c16n + ci0 / 16) * 6;
-        for (int j = wave; j < WLI; j += 4) {
+#pragma unroll
+        for (int jw = 0; jw < WIW; ++jw) {
+            int j = wave + 4 * jw;
+            if (j >= WLI) j -= WLI;  // wave-uniform
             const int L = j * 64 + lane;
             const int run = L / BO, o = L - run * BO;   // run = chunk * 6 + term * 2 + octet
             const short* src = wx + ((wbase + run) * p.cout + o0 + o) * 8;
@@ -784,15 +800,29 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
 
     const int kh = lane >> 5, l32 = lane & 31;
     int issued = ks_begin;
-    if (issued < ks_end) {
-        issue(issued, 0);
-        ++issued;
+#pragma unroll
+    for (int q = 0; q < NST - 1; ++q) {
+        if (issued < ks_end) {
+            issue(issued, (issued - ks_begin) % NST);
+            ++issued;
+        }
     }
     for (int ks = ks_begin; ks < ks_end; ++ks) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // every wave's DMAs for step ks have landed; the other slot is free
+        // this wave's DMAs for step ks are done once at most (issued - ks - 1) later steps remain in flight
+        const int ahead = issued - ks - 1;
+        if constexpr (NST == 2) {
+            wait_vmcnt<0>();
+        } else if constexpr (NST == 3) {
+            if (ahead >= 1) wait_vmcnt<PER>();
+            else wait_vmcnt<0>();
+        } else {
+            if (ahead >= 2) wait_vmcnt<2 * PER>();
+            else if (ahead == 1) wait_vmcnt<PER>();
+            else wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's DMAs for step ks have landed; slot ks-1 is free
         asm volatile("" ::: "memory");
-        const int slot = (ks - ks_begin) & 1;
+        const int slot = (ks - ks_begin) % NST;
         const char* st = smem + slot * STAGE;
         const short* Wp = reinterpret_cast<const short*>(st);
         const float* Xs = reinterpret_cast<const float*>(st + WB);
@@ -814,8 +844,8 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
                     at[i][s] = *reinterpret_cast<const bf16x8*>(
                         Wp + ((((kc * 3 + s) * 2 + kh) * BO) + wo * TO * 32 + i * 32 + l32) * 8);
             __builtin_amdgcn_sched_barrier(0);
-            if (kc == 0 && issued < ks_end) {  // the next step's DMAs under this step's MFMAs
-                issue(issued, (issued - ks_begin) & 1);
+            if (kc == 0 && issued < ks_end) {  // a later step's DMAs under this step's MFMAs
+                issue(issued, (issued - ks_begin) % NST);
                 ++issued;
             }
 #pragma unroll
@@ -2061,6 +2091,8 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         RowTaps rt{};
         if (x3) {
             const bool k32 = cfg == 0 && lds_bk32(cfg, cin);
+            // 32-channel K steps for the narrow tiles too (A/B knob SMC_X3_K32_SMALL: half the barriers per FLOP)
+            const bool k32s = SMC_X3_K32_SMALL && cin % 32 == 0;
             if (cfg == 0 && k32 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32, 1>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0 && k32) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 16, 1>), grid, dim3(NT), 0, st, p);
@@ -2068,8 +2100,11 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             else if (cfg == 3 && cin % 32 == 0 && tag)
                 hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 32, 1>), grid, dim3(NT), 0, st, p);
             else if (cfg == 3 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 16, 1>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 3 && k32s) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 32>), grid, dim3(NT), 0, st, p);
             else if (cfg == 3) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 16>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 4 && k32s) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 1, 1, 32>), grid, dim3(NT), 0, st, p);
             else if (cfg == 4) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 1, 1, 16>), grid, dim3(NT), 0, st, p);
+            else if (k32s) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 2, 32>), grid, dim3(NT), 0, st, p);
             else hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 2, 16>), grid, dim3(NT), 0, st, p);
             rc = smc::check_launch("smc_conv_gemm_f32 (split-bf16)");
             if (rc != SMC_OK || nsplit == 1) return rc;
