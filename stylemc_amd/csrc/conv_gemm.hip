@@ -685,7 +685,7 @@ __global__ __launch_bounds__(256) void x3_weights_kernel(const float* wk, const 
 #define SMC_X3_NST 2
 #endif
 #ifndef SMC_X3_K32_SMALL
-#define SMC_X3_K32_SMALL 0
+#define SMC_X3_K32_SMALL 1
 #endif
 
 template <int WO, int WM, int TO, int TM, int BKT, int TAG = 0, int NST = SMC_X3_NST>
