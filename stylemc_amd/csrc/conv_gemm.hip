@@ -688,7 +688,7 @@ __global__ __launch_bounds__(256) void x3_weights_kernel(const float* wk, const 
 #define SMC_X3_K32_SMALL 1
 #endif
 
-template <int WO, int WM, int TO, int TM, int BKT, int TAG = 0, int NST = SMC_X3_NST>
+template <int WO, int WM, int TO, int TM, int BKT, int NST = SMC_X3_NST, int TAG = 0>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
     static_assert(WO * WM == 4, "4 waves");
     static_assert(BKT % 16 == 0, "16-channel chunks");
@@ -2093,13 +2093,13 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             const bool k32 = cfg == 0 && lds_bk32(cfg, cin);
             // 32-channel K steps for the narrow tiles too (A/B knob SMC_X3_K32_SMALL: half the barriers per FLOP)
             const bool k32s = SMC_X3_K32_SMALL && cin % 32 == 0;
-            if (cfg == 0 && k32 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32, 1>), grid, dim3(NT), 0, st, p);
+            if (cfg == 0 && k32 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0 && k32) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32>), grid, dim3(NT), 0, st, p);
-            else if (cfg == 0 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 16, 1>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 0 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 16, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 16>), grid, dim3(NT), 0, st, p);
             else if (cfg == 3 && cin % 32 == 0 && tag)
-                hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 32, 1>), grid, dim3(NT), 0, st, p);
-            else if (cfg == 3 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 16, 1>), grid, dim3(NT), 0, st, p);
+                hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 32, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 3 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 16, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
             else if (cfg == 3 && k32s) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 32>), grid, dim3(NT), 0, st, p);
             else if (cfg == 3) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 1, 1, 16>), grid, dim3(NT), 0, st, p);
             else if (cfg == 4 && k32s) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 1, 1, 32>), grid, dim3(NT), 0, st, p);

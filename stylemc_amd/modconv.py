@@ -154,7 +154,8 @@ def gemm(x, y, phases, nph, cin, cout, s=None, epi=None, alg_flops=0.0, alg_byte
     ws_bytes = lib.smc_conv_gemm_workspace_size(n, cin, cout, yh, yw, phases, nph)
     ws = torch.empty(max(ws_bytes // 4, 1), device=x.device, dtype=torch.float32) if ws_bytes > 0 else None
     tm = _hip.timer()
-    tok = tm.wrap(alg_flops, alg_bytes) if tm is not None else None
+    kind = "direct_x3" if all(phases[i].wk_x3 for i in range(nph)) else "direct"
+    tok = tm.wrap(alg_flops, alg_bytes, kind=kind) if tm is not None else None
     _hip.call("smc_conv_gemm_f32", x.data_ptr(), n, cin, ih, iw, y.data_ptr(), cout, yh, yw, phases, nph,
               _hip.ptr(s), ctypes.byref(epi) if epi is not None else None, _hip.ptr(ws), ws_bytes, _hip.stream())
     if tok is not None:

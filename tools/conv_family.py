@@ -3,7 +3,7 @@ smc_conv_gemm_f32 / smc_conv3x3_wino_f32 / smc_conv3x3_wino4_f32 launch for the 
 the same GEMM kernels carry TAG 1 (a trailing ", 1>" template argument) and are not part of it."""
 
 FAMILY = ("conv_gemm_lds_kernel", "conv_gemm_kernel", "conv_row_kernel", "convt_gemm_kernel", "convt_lds_kernel",
-          "wino_kernel", "wino4_kernel")
+          "conv_gemm_x3_kernel", "convt_x3_kernel", "wino_kernel", "wino4_kernel")
 
 
 def is_family(name):
