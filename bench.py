@@ -89,6 +89,8 @@ def parse():
     p.add_argument("--conv-products", default="x3", choices=["x3", "fp32"],
                    help="direct implicit-GEMM convs: x3 = fp32 products as three-term bf16 splits (six bf16 MFMAs, "
                         "fp32-class error), fp32 = the exact-fp32 MFMA (modconv.X3)")
+    p.add_argument("--vit-products", default="x3", choices=["x3", "fp32"],
+                   help="CLIP ViT projections: split-bf16 (x3) or exact-fp32 MFMA GEMMs (vit_hip.X3)")
     p.add_argument("--schedule", default="prefetch", choices=["pair", "prefetch"],
                    help="stream schedule: pair = original synthesis beside the edited one; prefetch = the next "
                         "iteration's original synthesis on a third stream (DESIGN.md section 6b)")
@@ -324,6 +326,8 @@ def main():
     from stylemc_amd.id_loss import IDLoss
     from stylemc_amd import modconv, synthetic
     modconv.X3 = args.conv_products == "x3"
+    from stylemc_amd import vit_hip
+    vit_hip.X3 = args.vit_products == "x3"
 
     G = load_generator("synthetic", args.resolution, dev)
     # weak scaling: 129 seeds per GPU and a global batch of 4 per GPU give every N the single-GPU schedule
@@ -454,7 +458,7 @@ def main():
                    "n_seeds": n_seeds, "seeds_per_gpu": n_seeds / world.world_size,
                    "parallelism": f"dp{world.world_size}", "clip_type": args.clip_type, "clip_impl": args.clip_impl, "id_impl": args.id_impl,
                    "batched_loss_pairs": finder.batch_losses, "landmarks_loss_coef": 0,
-                   "conv_products": args.conv_products,
+                   "conv_products": args.conv_products, "vit_products": args.vit_products,
                    "direction_finite": finite, "world_size": world.world_size, "backend": world.backend,
                    "launcher": (os.environ.get("SMC_BENCH_LAUNCHER", "torch.distributed.run")
                                 if world.world_size > 1 else None),

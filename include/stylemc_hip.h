@@ -331,6 +331,8 @@ int smc_patch_im2col_f32(const float* img, float* patches, int batch, int channe
 typedef struct {
     int width, layers, heads, patch, grid, out_dim, in_ch; /* ViT-B/32: 768, 12, 12, 32, 7, 512, 3 */
     float ln_eps;                                          /* 1e-5 (nn.LayerNorm default)          */
+    int products;  /* 0: exact-fp32 MFMA; 1: split-bf16 (three bf16 terms per fp32 operand, the six products above
+                      2^-23 |a b|; the packed buffer then ends with every projection's planes, smc_vit_pack_x3) */
 } smc_vit_config;
 
 /* Packed frozen weights: one fp32 buffer, segments in this order, each padded to 64 floats:
@@ -345,6 +347,8 @@ typedef struct {
 int64_t smc_vit_packed_floats(const smc_vit_config* cfg);
 /* Activations the backward needs, per batch size (floats). */
 int64_t smc_vit_saved_floats(const smc_vit_config* cfg, int batch);
+/* products = 1: fill the planes region at the end of `packed` from its fp32 segments (after they are written). */
+int smc_vit_pack_x3(const smc_vit_config* cfg, float* packed, void* stream);
 int64_t smc_vit_workspace_bytes(const smc_vit_config* cfg, int batch);
 /* image [batch][in_ch][grid*patch][grid*patch] -> out [batch][out_dim]; saved may be NULL (no backward). */
 int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, const float* image, int batch, float* out,

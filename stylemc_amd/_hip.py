@@ -41,7 +41,7 @@ class LinearEpilogue(ctypes.Structure):
 
 class VitConfig(ctypes.Structure):
     _fields_ = [("width", c_int), ("layers", c_int), ("heads", c_int), ("patch", c_int), ("grid", c_int),
-                ("out_dim", c_int), ("in_ch", c_int), ("ln_eps", c_float)]
+                ("out_dim", c_int), ("in_ch", c_int), ("ln_eps", c_float), ("products", c_int)]
 
 
 LIN_ACT_NONE, LIN_ACT_QUICKGELU = 0, 1
@@ -98,6 +98,7 @@ _SIGS = {
     "smc_patch_im2col_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "smc_vit_packed_floats": (c_int64, [P]),
     "smc_vit_saved_floats": (c_int64, [P, c_int]),
+    "smc_vit_pack_x3": (c_int, [P, P, P]),
     "smc_vit_workspace_bytes": (c_int64, [P, c_int]),
     "smc_vit_forward_f32": (c_int, [P, P, P, c_int, P, P, P, c_int64, P]),
     "smc_vit_backward_f32": (c_int, [P, P, P, c_int, c_int, P, P, P, c_int64, P]),

@@ -399,6 +399,208 @@ __global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, 
     }
 }
 
+// ------------------------------------------------------------------------------------------ GEMM, split-bf16
+// lin_gemm2_kernel with the fp32 products as three-term bf16 splits on v_mfma_f32_16x16x32_bf16 (the scheme of
+// conv_gemm.hip's conv_gemm_x3_kernel: a = a0 + a1 + a2 exactly, six products a_i b_j with i + j <= 2, error per
+// product <= 2^-23 |a b|).  Same 32 x 64 tiles, 2-stage DMA ring, XCD order, split-K hand-off and epilogue; the
+// frozen B operand comes pre-split as planes [K/32][3][4][N][8] bf16 (lin_x3_planes_kernel), so a B fragment (8
+// consecutive k of one column) is one conflict-free ds_read_b128 per term; the A tile stays fp32 (its XOR-swizzled
+// image of lin_gemm2_kernel) and each wave splits its A fragment (8 consecutive k of one row) in registers, once for
+// the wave's two column blocks.
+typedef short bf16x8v __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void lin_split8(const float (&x)[8], bf16x8v (&t)[3]) {
+    unsigned u0[8], u1[8], u2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const unsigned u = __float_as_uint(x[j]);
+        const float r1 = x[j] - __uint_as_float(u & 0xffff0000u);
+        const unsigned v = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(v & 0xffff0000u);
+        u0[j] = u;
+        u1[j] = v;
+        u2[j] = __float_as_uint(r2);
+    }
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 w0, w1, w2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        w0[j] = __builtin_amdgcn_perm(u0[2 * j + 1], u0[2 * j], 0x07060302u);
+        w1[j] = __builtin_amdgcn_perm(u1[2 * j + 1], u1[2 * j], 0x07060302u);
+        w2[j] = __builtin_amdgcn_perm(u2[2 * j + 1], u2[2 * j], 0x07060302u);
+    }
+    t[0] = __builtin_bit_cast(bf16x8v, w0);
+    t[1] = __builtin_bit_cast(bf16x8v, w1);
+    t[2] = __builtin_bit_cast(bf16x8v, w2);
+}
+
+// planes of a row-major [K][N] fp32 matrix (ldb floats per row): term s of b[k][n] at
+// ((((k / 32) * 3 + s) * 4 + (k % 32) / 8) * N + n) * 8 + k % 8
+__global__ __launch_bounds__(256) void lin_x3_planes_kernel(const float* b, int ldb, int K, int N, short* out) {
+    const int64_t total = (int64_t)K * N;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int ke = (int)(e & 7);
+        int64_t r = e >> 3;
+        const int n = (int)(r % N);
+        r /= N;
+        const int g = (int)(r & 3);
+        const int kb = (int)(r >> 2);
+        const int k = kb * 32 + g * 8 + ke;
+        const float v = b[(int64_t)k * ldb + n];
+        const unsigned u = __float_as_uint(v);
+        const float r1 = v - __uint_as_float(u & 0xffff0000u);
+        const unsigned w = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(w & 0xffff0000u);
+        const unsigned term[3] = {u >> 16, w >> 16, __float_as_uint(r2) >> 16};
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+            out[((((int64_t)kb * 3 + s) * 4 + g) * N + n) * 8 + ke] = (short)term[s];
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void lin_gemm2_x3_kernel(LinParams p, const short* bx3, int mt, int ntl) {
+    constexpr int ABYTES = L2M * L2K * 4;               // A tile [32][64] fp32
+    constexpr int BBYTES = (L2K / 32) * 12 * L2N * 16;  // B planes [2][3][4][64][8] bf16
+    constexpr int STAGE = ABYTES + BBYTES;
+    constexpr int BDMA = BBYTES / 1024;                 // 24 1-KB DMAs, 6 per wave
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int nb = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
+    const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int m_tile = lin % mt;
+    const int rest = lin / mt;
+    const int n_tile = rest % ntl;
+    const int split = rest / ntl;
+    const int m0 = m_tile * L2M, n0 = n_tile * L2N;
+    const int nks = p.K / L2K;
+    const int ks0 = (int)((int64_t)nks * split / p.nsplit);
+    const int ks1 = (int)((int64_t)nks * (split + 1) / p.nsplit);
+
+    auto issue = [&](int ks, int slot) {
+        char* st = smem + slot * STAGE;
+        float* As = reinterpret_cast<float*>(st);
+        const int k0 = ks * L2K;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {  // A: as lin_gemm2_kernel
+            const int base = (wave * 2 + j) * 256;
+            const int v = base / 4 + lane;
+            const int row = v >> 4, cphys = v & 15;
+            const int c = cphys ^ (row & 15);
+            const int grow = min(m0 + row, p.M - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(p.a + (int64_t)grow * p.lda + k0 + 4 * c),
+                                             (__attribute__((address_space(3))) void*)(As + base), 16, 0, 0);
+        }
+        // B planes: lane L of the step's 1536 16-B lanes -> (chunk kc, run = term * 4 + octet, column n)
+#pragma unroll
+        for (int j = 0; j < BDMA / 4; ++j) {
+            const int jj = wave * (BDMA / 4) + j;
+            const int L = jj * 64 + lane;
+            const int kc = L / (12 * L2N), rem = L - kc * (12 * L2N);
+            const int run = rem / L2N, n = rem - run * L2N;
+            const short* src = bx3 + ((((int64_t)(k0 / 32 + kc) * 12 + run) * p.N) + n0 + n) * 8;
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(st + ABYTES + jj * 1024), 16, 0, 0);
+        }
+    };
+
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const int i = lane & 15, g = lane >> 4;
+    const int arow = wm * 16 + i;
+    if (ks0 < ks1) issue(ks0, 0);
+    for (int ks = ks0; ks < ks1; ++ks) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (ks + 1 < ks1) issue(ks + 1, (ks + 1 - ks0) & 1);
+        const char* st = smem + ((ks - ks0) & 1) * STAGE;
+        const float* As = reinterpret_cast<const float*>(st);
+        const short* Bs = reinterpret_cast<const short*>(st + ABYTES);
+#pragma unroll
+        for (int kc = 0; kc < L2K / 32; ++kc) {
+            const int c0 = kc * 8 + 2 * g;  // float4 columns of k = 32 kc + 8 g .. + 7
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(As + arow * L2K + 4 * (c0 ^ (arow & 15)));
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(As + arow * L2K + 4 * ((c0 + 1) ^ (arow & 15)));
+            const float xv[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+            bf16x8v at[3], bt[2][3];
+            lin_split8(xv, at);
+#pragma unroll
+            for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+                for (int s = 0; s < 3; ++s)
+                    bt[blk][s] = *reinterpret_cast<const bf16x8v*>(
+                        Bs + (((kc * 3 + s) * 4 + g) * L2N + wn * 32 + blk * 16 + i) * 8);
+#pragma unroll
+            for (int blk = 0; blk < 2; ++blk) {
+                acc[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[2], bt[blk][0], acc[blk], 0, 0, 0);
+                acc[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[1], bt[blk][1], acc[blk], 0, 0, 0);
+                acc[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[0], bt[blk][2], acc[blk], 0, 0, 0);
+                acc[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[1], bt[blk][0], acc[blk], 0, 0, 0);
+                acc[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[0], bt[blk][1], acc[blk], 0, 0, 0);
+                acc[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[0], bt[blk][0], acc[blk], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    // epilogue and split-K hand-off: as lin_gemm2_kernel (the 16x16x32 C layout is the 16x16x4 one)
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+        const int n = n0 + wn * 32 + blk * 16 + i;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int m = m0 + wm * 16 + 4 * g + rr;
+            if (m >= p.M) continue;
+            if (p.nsplit == 1)
+                p.c[(int64_t)m * p.ldc + n] = lin_epi(acc[blk][rr], m, n, p.e);
+            else if (p.counters)
+                __hip_atomic_store(p.ws + ((int64_t)split * p.M + m) * p.N + n, acc[blk][rr], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            else
+                p.ws[((int64_t)split * p.M + m) * p.N + n] = acc[blk][rr];
+        }
+    }
+    if (p.nsplit == 1 || !p.counters) return;
+    int* flag = reinterpret_cast<int*>(smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const int prev = __hip_atomic_fetch_add(p.counters + n_tile * mt + m_tile, 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == p.nsplit - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    float v[2][4];
+    for (int k = 0; k < p.nsplit; ++k) {
+        const float* part = p.ws + (int64_t)k * p.M * p.N;
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int m = min(m0 + wm * 16 + 4 * g + rr, p.M - 1);
+                const float t = part[(int64_t)m * p.N + n0 + wn * 32 + blk * 16 + i];
+                v[blk][rr] = k == 0 ? t : v[blk][rr] + t;
+            }
+    }
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+        const int n = n0 + wn * 32 + blk * 16 + i;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int m = m0 + wm * 16 + 4 * g + rr;
+            if (m < p.M) p.c[(int64_t)m * p.ldc + n] = lin_epi(v[blk][rr], m, n, p.e);
+        }
+    }
+}
+
 bool lin_v2_ok(int N, int K, int lda, int ldb) {
     return K % L2K == 0 && N % L2N == 0 && lda % 4 == 0 && ldb % 4 == 0;
 }
@@ -426,7 +628,8 @@ int64_t lin_ws_floats(int M, int N, int K) {
 }
 
 int lin_launch(const float* a, int lda, const float* b, int ldb, float* c, int ldc, int M, int N, int K,
-               const smc_linear_epilogue* epi, float* ws, int64_t ws_bytes, hipStream_t st, int* counters = nullptr) {
+               const smc_linear_epilogue* epi, float* ws, int64_t ws_bytes, hipStream_t st, int* counters = nullptr,
+               const short* bx3 = nullptr) {
     int rc = lin_validate(a, lda, b, ldb, c, ldc, M, N, K);
     if (rc != SMC_OK) return rc;
     LinParams p{};
@@ -441,7 +644,10 @@ int lin_launch(const float* a, int lda, const float* b, int ldb, float* c, int l
         p.ws = ws;
         p.counters = counters;
     }
-    if (v2) {
+    if (v2 && bx3) {  // split-bf16 products (B given as planes over the same [K][N])
+        const int mt = (int)smc::ceil_div(M, L2M), ntl = N / L2N;
+        hipLaunchKernelGGL(lin_gemm2_x3_kernel, dim3((unsigned)(mt * ntl * p.nsplit)), dim3(256), 0, st, p, bx3, mt, ntl);
+    } else if (v2) {
         const int mt = (int)smc::ceil_div(M, L2M), ntl = N / L2N;
         hipLaunchKernelGGL(lin_gemm2_kernel, dim3((unsigned)(mt * ntl * p.nsplit)), dim3(256), 0, st, p, mt, ntl);
     } else {
@@ -827,6 +1033,7 @@ inline int64_t rnd(int64_t n) { return (n + 63) & ~int64_t(63); }
 
 struct VitDims {
     int D, NL, H, p, G, E, C, L, P;  // P = C*p*p
+    int x3;                          // split-bf16 products: the packed buffer also holds every projection's planes
 };
 
 VitDims dims(const smc_vit_config& c) {
@@ -834,19 +1041,28 @@ VitDims dims(const smc_vit_config& c) {
     d.D = c.width; d.NL = c.layers; d.H = c.heads; d.p = c.patch; d.G = c.grid; d.E = c.out_dim; d.C = c.in_ch;
     d.L = c.grid * c.grid + 1;
     d.P = c.in_ch * c.patch * c.patch;
+    d.x3 = c.products == 1;
     return d;
 }
 
 struct LayerW {
     const float *ln1_w, *ln1_b, *qkv_wt, *qkv_w, *qkv_b, *out_wt, *out_w, *out_b, *ln2_w, *ln2_b, *fc_wt, *fc_w,
         *fc_b, *pr_wt, *pr_w, *pr_b;
+    // split-bf16 planes of the eight projections (nullptr: exact-fp32 products)
+    const short *qkv_wt3, *qkv_w3, *out_wt3, *out_w3, *fc_wt3, *fc_w3, *pr_wt3, *pr_w3;
 };
 
 struct VitW {
     const float *conv_wt, *conv_w, *cls, *pos, *lnpre_w, *lnpre_b, *lnpost_w, *lnpost_b, *proj, *proj_t;
     const float* layers;  // start of layer 0
     int64_t layer_stride;
+    const short *conv_wt3, *conv_w3, *proj3, *proj_t3;
+    const float* layers3;  // start of layer 0's planes
+    int64_t layer3_stride;
 };
+
+// floats of the split planes of a [K][N] matrix (3 bf16 terms per element), 64-float aligned
+inline int64_t planes_floats(int64_t K, int64_t N) { return (K * N * 3 + 1) / 2; }
 
 int64_t layer_floats(const VitDims& d) {
     const int64_t D = d.D;
@@ -877,6 +1093,17 @@ int64_t layout(const VitDims& d, const float* base, VitW* w) {
     t.lnpost_b = seg(D);
     t.proj = seg(D * d.E);
     t.proj_t = seg((int64_t)d.E * D);
+    if (d.x3) {  // the planes region after the fp32 segments (smc_vit_pack_x3 fills it from them)
+        auto pseg = [&](int64_t K, int64_t N) { return reinterpret_cast<const short*>(seg(planes_floats(K, N))); };
+        t.conv_wt3 = pseg(d.P, D);
+        t.conv_w3 = pseg(D, d.P);
+        t.layers3 = base ? base + off : nullptr;
+        t.layer3_stride = rnd(planes_floats(D, 3 * D)) + rnd(planes_floats(3 * D, D)) + 2 * rnd(planes_floats(D, D)) +
+                          2 * rnd(planes_floats(D, 4 * D)) + 2 * rnd(planes_floats(4 * D, D));
+        off += t.layer3_stride * d.NL;
+        t.proj3 = pseg(D, d.E);
+        t.proj_t3 = pseg(d.E, D);
+    }
     if (w) *w = t;
     return off;
 }
@@ -897,6 +1124,21 @@ LayerW layer_w(const VitDims& d, const VitW& w, int l) {
     t.ln2_w = seg(D); t.ln2_b = seg(D);
     t.fc_wt = seg(D * 4 * D); t.fc_w = seg(4 * D * D); t.fc_b = seg(4 * D);
     t.pr_wt = seg(4 * D * D); t.pr_w = seg(D * 4 * D); t.pr_b = seg(D);
+    t.qkv_wt3 = t.qkv_w3 = t.out_wt3 = t.out_w3 = t.fc_wt3 = t.fc_w3 = t.pr_wt3 = t.pr_w3 = nullptr;
+    if (d.x3) {
+        const float* b3 = w.layers3 + w.layer3_stride * l;
+        int64_t o3 = 0;
+        auto pseg = [&](int64_t K, int64_t N) {
+            const short* ptr = reinterpret_cast<const short*>(b3 + o3);
+            o3 += rnd(planes_floats(K, N));
+            return ptr;
+        };
+        // [K][N] of each B operand: forward W^T [in][out], backward W [out][in]
+        t.qkv_wt3 = pseg(D, 3 * D); t.qkv_w3 = pseg(3 * D, D);
+        t.out_wt3 = pseg(D, D); t.out_w3 = pseg(D, D);
+        t.fc_wt3 = pseg(D, 4 * D); t.fc_w3 = pseg(4 * D, D);
+        t.pr_wt3 = pseg(4 * D, D); t.pr_w3 = pseg(D, 4 * D);
+    }
     return t;
 }
 
@@ -1025,6 +1267,8 @@ int vit_validate(const smc_vit_config* cfg, int B) {
     SMC_CHECK(cfg->width >= 64 && cfg->layers >= 1 && cfg->heads >= 1 && cfg->patch >= 1 && cfg->grid >= 1 &&
                   cfg->out_dim >= 4 && cfg->in_ch >= 1,
               "smc_vit: bad config");
+    SMC_CHECK(cfg->products == 0 || cfg->products == 1, "smc_vit: products %d (0: fp32 MFMA, 1: split-bf16)",
+              cfg->products);
     if (cfg->width != cfg->heads * HD || cfg->width % 64 != 0 || cfg->width > 64 * LN_MAXV ||
         (cfg->in_ch * cfg->patch * cfg->patch) % LBK != 0 || cfg->width % LBK != 0 || cfg->out_dim % LBK != 0) {
         smc::set_error("smc_vit: unsupported config (head dim must be 64, width %% 64 == 0 <= 1024, "
@@ -1125,6 +1369,38 @@ SMC_API int64_t smc_vit_packed_floats(const smc_vit_config* cfg) {
     return layout(dims(*cfg), nullptr, nullptr);
 }
 
+SMC_API int smc_vit_pack_x3(const smc_vit_config* cfg, float* packed, void* stream) {
+    SMC_TRY(vit_validate(cfg, 1));
+    SMC_CHECK(packed, "smc_vit_pack_x3: null pointer");
+    const VitDims d = dims(*cfg);
+    SMC_CHECK(d.x3, "smc_vit_pack_x3: config has products = 0 (no planes region)");
+    VitW w;
+    layout(d, packed, &w);
+    hipStream_t st = smc::as_stream(stream);
+    auto planes = [&](const float* b, int K, int N, const short* out) {
+        const int64_t total = (int64_t)K * N;
+        hipLaunchKernelGGL(lin_x3_planes_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(total, 256), 8192)),
+                           dim3(256), 0, st, b, N, K, N, const_cast<short*>(out));
+    };
+    const int D = d.D;
+    planes(w.conv_wt, d.P, D, w.conv_wt3);
+    planes(w.conv_w, D, d.P, w.conv_w3);
+    for (int l = 0; l < d.NL; ++l) {
+        const LayerW lw = layer_w(d, w, l);
+        planes(lw.qkv_wt, D, 3 * D, lw.qkv_wt3);
+        planes(lw.qkv_w, 3 * D, D, lw.qkv_w3);
+        planes(lw.out_wt, D, D, lw.out_wt3);
+        planes(lw.out_w, D, D, lw.out_w3);
+        planes(lw.fc_wt, D, 4 * D, lw.fc_wt3);
+        planes(lw.fc_w, 4 * D, D, lw.fc_w3);
+        planes(lw.pr_wt, 4 * D, D, lw.pr_wt3);
+        planes(lw.pr_w, D, 4 * D, lw.pr_w3);
+    }
+    planes(w.proj, D, d.E, w.proj3);
+    planes(w.proj_t, d.E, D, w.proj_t3);
+    return smc::check_launch("smc_vit_pack_x3");
+}
+
 SMC_API int64_t smc_vit_saved_floats(const smc_vit_config* cfg, int batch) {
     if (vit_validate(cfg, batch) != SMC_OK) return -1;
     return saved_layout(dims(*cfg), batch, nullptr, nullptr);
@@ -1153,14 +1429,14 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
     const float eps = cfg->ln_eps;
     int64_t cursor = 0;
     auto lin = [&](const float* a, int lda, const float* bw, int ldb, float* c, int ldc, int MM, int N, int K,
-                   const smc_linear_epilogue& e) {
+                   const smc_linear_epilogue& e, const short* bx3) {
         int* ctr = ws.counters + cursor;
         cursor += ws.counter_slice;
         if (cursor > ws.counter_ints) {
             smc::set_error("smc_vit: split-K counter slices exhausted");
             return SMC_ERR_INVALID;
         }
-        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr);
+        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr, bx3);
     };
     if (hipMemsetAsync(ws.counters, 0, sizeof(int) * (size_t)ws.counter_ints, st) != hipSuccess) {
         smc::set_error("smc_vit: counter memset failed");
@@ -1169,7 +1445,7 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
 
     // patch embedding + class token + positional embedding, ln_pre
     SMC_TRY(smc_patch_im2col_f32(image, ws.patches, B, d.C, d.G, d.p, 0, stream));
-    SMC_TRY(lin(ws.patches, d.P, w.conv_wt, D, ws.tok, D, Mt, D, d.P, epi_none()));
+    SMC_TRY(lin(ws.patches, d.P, w.conv_wt, D, ws.tok, D, Mt, D, d.P, epi_none(), w.conv_wt3));
     float* x_pre = saved ? sv.x_pre : ws.xb;
     hipLaunchKernelGGL(embed_fwd_kernel, dim3(ew_blocks((int64_t)M * D)), dim3(256), 0, st, ws.tok, w.cls, w.pos,
                        x_pre, B, d.L, D);
@@ -1192,13 +1468,13 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
                               saved ? ls.rs1 : nullptr, M, D, eps, st));
         smc_linear_epilogue e = epi_none();
         e.bias = lw.qkv_b;
-        SMC_TRY(lin(ws.h, D, lw.qkv_wt, 3 * D, qkv, 3 * D, M, 3 * D, D, e));
+        SMC_TRY(lin(ws.h, D, lw.qkv_wt, 3 * D, qkv, 3 * D, M, 3 * D, D, e, lw.qkv_wt3));
         SMC_TRY(attn_fwd_launch(qkv, ws.o, saved ? ls.P : nullptr, B, d.L, d.H, scale, st));
         e = epi_none();
         e.bias = lw.out_b;
         e.residual = x_in;
         e.ld_res = D;
-        SMC_TRY(lin(ws.o, D, lw.out_wt, D, x_mid, D, M, D, D, e));
+        SMC_TRY(lin(ws.o, D, lw.out_wt, D, x_mid, D, M, D, D, e, lw.out_wt3));
         // MLP block: x_out = x_mid + c_proj(QuickGELU(c_fc(ln_2(x_mid))))
         SMC_TRY(ln_fwd_launch(x_mid, D, lw.ln2_w, lw.ln2_b, ws.h, D, saved ? ls.mu2 : nullptr,
                               saved ? ls.rs2 : nullptr, M, D, eps, st));
@@ -1207,18 +1483,18 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
         e.act = SMC_LIN_ACT_QUICKGELU;
         e.pre_save = saved ? ls.G : nullptr;
         e.ld_pre = 4 * D;
-        SMC_TRY(lin(ws.h, D, lw.fc_wt, 4 * D, ws.big, 4 * D, M, 4 * D, D, e));
+        SMC_TRY(lin(ws.h, D, lw.fc_wt, 4 * D, ws.big, 4 * D, M, 4 * D, D, e, lw.fc_wt3));
         e = epi_none();
         e.bias = lw.pr_b;
         e.residual = x_mid;
         e.ld_res = D;
-        SMC_TRY(lin(ws.big, 4 * D, lw.pr_wt, D, x_out, D, M, D, 4 * D, e));
+        SMC_TRY(lin(ws.big, 4 * D, lw.pr_wt, D, x_out, D, M, D, 4 * D, e, lw.pr_wt3));
         x = x_out;
     }
     // head: ln_post(x[:, 0]) @ proj   (CLS rows, stride L*D)
     SMC_TRY(ln_fwd_launch(x, (int64_t)d.L * D, w.lnpost_w, w.lnpost_b, ws.h, D, saved ? sv.mupost : nullptr,
                           saved ? sv.rspost : nullptr, B, D, eps, st));
-    return lin(ws.h, D, w.proj, d.E, out, d.E, B, d.E, D, epi_none());
+    return lin(ws.h, D, w.proj, d.E, out, d.E, B, d.E, D, epi_none(), w.proj3);
 }
 
 SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed, const float* dout, int batch,
@@ -1243,14 +1519,14 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
     saved_layout(d, batch, const_cast<float*>(saved), &sv);
     int64_t cursor = 0;
     auto lin = [&](const float* a, int lda, const float* bw, int ldb, float* c, int ldc, int MM, int N, int K,
-                   const smc_linear_epilogue& e) {
+                   const smc_linear_epilogue& e, const short* bx3) {
         int* ctr = ws.counters + cursor;
         cursor += ws.counter_slice;
         if (cursor > ws.counter_ints) {
             smc::set_error("smc_vit: split-K counter slices exhausted");
             return SMC_ERR_INVALID;
         }
-        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr);
+        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr, bx3);
     };
     if (hipMemsetAsync(ws.counters, 0, sizeof(int) * (size_t)ws.counter_ints, st) != hipSuccess) {
         smc::set_error("smc_vit: counter memset failed");
@@ -1258,7 +1534,7 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
     }
 
     // head: d(ln_post out) = dout @ proj^T, then ln_post backward into the CLS rows of a zeroed dx
-    SMC_TRY(lin(dout, d.E, w.proj_t, D, ws.h, D, B, D, d.E, epi_none()));
+    SMC_TRY(lin(dout, d.E, w.proj_t, D, ws.h, D, B, D, d.E, epi_none(), w.proj_t3));
     if (hipMemsetAsync(ws.dx, 0, sizeof(float) * (size_t)M * D, st) != hipSuccess) {
         smc::set_error("smc_vit_backward_f32: memset failed");
         return SMC_ERR_LAUNCH;
@@ -1275,19 +1551,19 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
         smc_linear_epilogue e = epi_none();
         e.dact_pre = ls.G;
         e.ld_dact = 4 * D;
-        SMC_TRY(lin(dx, D, lw.pr_w, 4 * D, ws.big, 4 * D, M, 4 * D, D, e));   // dG = (dx @ W_proj) * gelu'(G)
-        SMC_TRY(lin(ws.big, 4 * D, lw.fc_w, D, ws.dh, D, M, D, 4 * D, epi_none()));  // dh2 = dG @ W_fc
+        SMC_TRY(lin(dx, D, lw.pr_w, 4 * D, ws.big, 4 * D, M, 4 * D, D, e, lw.pr_w3));   // dG = (dx @ W_proj) * gelu'(G)
+        SMC_TRY(lin(ws.big, 4 * D, lw.fc_w, D, ws.dh, D, M, D, 4 * D, epi_none(), lw.fc_w3));  // dh2 = dG @ W_fc
         SMC_TRY(ln_bwd_launch(ws.dh, D, ls.x_mid, D, ls.mu2, ls.rs2, lw.ln2_w, dx, D, dx, D, M, D, st));
         // attention block
-        SMC_TRY(lin(dx, D, lw.out_w, D, ws.o, D, M, D, D, epi_none()));       // dO = dx_mid @ W_out
+        SMC_TRY(lin(dx, D, lw.out_w, D, ws.o, D, M, D, D, epi_none(), lw.out_w3));       // dO = dx_mid @ W_out
         SMC_TRY(attn_bwd_launch(ws.o, ls.qkv, ls.P, ws.qkv, B, d.L, d.H, scale, st));
-        SMC_TRY(lin(ws.qkv, 3 * D, lw.qkv_w, D, ws.dh, D, M, D, 3 * D, epi_none()));  // dh1 = dqkv @ W_in
+        SMC_TRY(lin(ws.qkv, 3 * D, lw.qkv_w, D, ws.dh, D, M, D, 3 * D, epi_none(), lw.qkv_w3));  // dh1 = dqkv @ W_in
         SMC_TRY(ln_bwd_launch(ws.dh, D, ls.x_in, D, ls.mu1, ls.rs1, lw.ln1_w, dx, D, dx, D, M, D, st));
     }
     // ln_pre backward, drop the class-token row, patch GEMM adjoint, col2im
     SMC_TRY(ln_bwd_launch(dx, D, sv.x_pre, D, sv.mu0, sv.rs0, w.lnpre_w, nullptr, 0, ws.dh, D, M, D, st));
     hipLaunchKernelGGL(embed_bwd_kernel, dim3(ew_blocks((int64_t)Mt * D)), dim3(256), 0, st, ws.dh, ws.tok, B, d.L, D);
     SMC_TRY(smc::check_launch("vit embed bwd"));
-    SMC_TRY(lin(ws.tok, D, w.conv_w, d.P, ws.patches, d.P, Mt, d.P, D, epi_none()));
+    SMC_TRY(lin(ws.tok, D, w.conv_w, d.P, ws.patches, d.P, Mt, d.P, D, epi_none(), w.conv_w3));
     return smc_patch_im2col_f32(dimage, ws.patches, B, d.C, d.G, d.p, 1, stream);
 }

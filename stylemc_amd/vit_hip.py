@@ -31,10 +31,17 @@ def _pad(t):
     return torch.cat([t, t.new_zeros(n - t.numel())])
 
 
-def vit_config(width, layers, heads, patch, grid, out_dim, in_ch=3, ln_eps=1e-5):
+# Split-bf16 products for the tower's projections (smc_vit_config.products = 1: three bf16 terms per fp32 operand, the
+# six products above 2^-23 |a b|; the weights' planes are built once at packing).  Module switch: tests compare it
+# against the exact-fp32 MFMA GEMMs.
+X3 = True
+
+
+def vit_config(width, layers, heads, patch, grid, out_dim, in_ch=3, ln_eps=1e-5, products=None):
     c = _hip.VitConfig()
     c.width, c.layers, c.heads, c.patch, c.grid, c.out_dim, c.in_ch, c.ln_eps = (width, layers, heads, patch, grid,
                                                                                   out_dim, in_ch, ln_eps)
+    c.products = (1 if X3 else 0) if products is None else int(products)
     return c
 
 
@@ -103,6 +110,14 @@ class _VitFn(torch.autograd.Function):
         return dimage, None, None
 
 
+def vit_config_like(cfg, **kw):
+    """A copy of a VitConfig with some fields replaced."""
+    c = _hip.VitConfig()
+    for name, _ in _hip.VitConfig._fields_:
+        setattr(c, name, kw.get(name, getattr(cfg, name)))
+    return c
+
+
 def ctypes_ref(cfg):
     import ctypes
     return ctypes.byref(cfg)
@@ -135,10 +150,20 @@ class HipVisionTransformer(nn.Module):
     def refresh(self):
         """Re-pack the frozen weights (after loading or moving them)."""
         packed = pack_weights(self.tower.state_dict(), self.layers)
-        n = _hip.load().smc_vit_packed_floats(ctypes_ref(self.cfg))
-        if n != packed.numel():
-            raise RuntimeError(f"packed ViT weights: {packed.numel()} floats, the library expects {n}")
-        self.packed = packed.to(self.tower.proj.device)
+        lib = _hip.load()
+        dev = self.tower.proj.device
+        if self.cfg.products == 1 and dev.type != "cuda":
+            self.cfg.products = 0  # (planes are built on the GPU; a CPU-resident tower keeps the fp32 layout)
+        fp32_part = lib.smc_vit_packed_floats(ctypes_ref(vit_config_like(self.cfg, products=0)))
+        if fp32_part != packed.numel():
+            raise RuntimeError(f"packed ViT weights: {packed.numel()} floats, the library expects {fp32_part}")
+        n = lib.smc_vit_packed_floats(ctypes_ref(self.cfg))
+        buf = torch.zeros(n, device=dev, dtype=torch.float32)
+        buf[:fp32_part].copy_(packed)
+        if self.cfg.products == 1:
+            _hip.call("smc_vit_pack_x3", ctypes_ref(self.cfg), buf.data_ptr(), _hip.stream())
+            torch.cuda.current_stream(dev).synchronize()
+        self.packed = buf
         return self
 
     def flops_per_image(self):

@@ -208,9 +208,18 @@ def _vit_pair(name, B, seed=4):
     return hip, ora, x, cot
 
 
+@pytest.fixture(params=[True, False], ids=["x3", "fp32"])
+def vit_x3(request, monkeypatch):
+    """Both product forms of the tower's projections: split-bf16 (vit_hip.X3, the default) and exact-fp32 MFMA."""
+    from stylemc_amd import vit_hip
+    monkeypatch.setattr(vit_hip, "X3", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("name,B", [("ViT-B/32", 4), ("ViT-B/32", 1), ("ViT-B/32", 8), ("ViT-B/16", 2)])
-def test_vit_forward_backward_vs_oracle(name, B):
+def test_vit_forward_backward_vs_oracle(name, B, vit_x3):
     hip, ora, x, cot = _vit_pair(name, B)
+    assert hip.cfg.products == (1 if vit_x3 else 0)
     xo = x.clone().requires_grad_(True)
     yo = ora(xo)
     (dxo,) = torch.autograd.grad(yo, xo, cot)
