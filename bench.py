@@ -89,7 +89,7 @@ def parse():
     p.add_argument("--conv-products", default="x3", choices=["x3", "fp32"],
                    help="direct implicit-GEMM convs: x3 = fp32 products as three-term bf16 splits (six bf16 MFMAs, "
                         "fp32-class error), fp32 = the exact-fp32 MFMA (modconv.X3)")
-    p.add_argument("--vit-products", default="x3", choices=["x3", "fp32"],
+    p.add_argument("--vit-products", default="fp32", choices=["x3", "fp32"],
                    help="CLIP ViT projections: split-bf16 (x3) or exact-fp32 MFMA GEMMs (vit_hip.X3)")
     p.add_argument("--schedule", default="prefetch", choices=["pair", "prefetch"],
                    help="stream schedule: pair = original synthesis beside the edited one; prefetch = the next "

@@ -32,9 +32,10 @@ def _pad(t):
 
 
 # Split-bf16 products for the tower's projections (smc_vit_config.products = 1: three bf16 terms per fp32 operand, the
-# six products above 2^-23 |a b|; the weights' planes are built once at packing).  Module switch: tests compare it
-# against the exact-fp32 MFMA GEMMs.
-X3 = True
+# six products above 2^-23 |a b|; the weights' planes are built once at packing).  Off by default: at 200..400 tokens
+# the projections are bound by re-reading the weights, and the planes are 1.5x the fp32 bytes -- measured 451.6 vs
+# 455.1 images/s with them on (profiles/r04/vit_ab/).  Module switch: tests run both forms.
+X3 = False
 
 
 def vit_config(width, layers, heads, patch, grid, out_dim, in_ch=3, ln_eps=1e-5, products=None):
