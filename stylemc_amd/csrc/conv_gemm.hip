@@ -687,6 +687,11 @@ __global__ __launch_bounds__(256) void x3_weights_kernel(const float* wk, const 
 #ifndef SMC_X3_K32_SMALL
 #define SMC_X3_K32_SMALL 1
 #endif
+// Timing probes only (0 in the library; tools/ builds a variant with SMC_AB_DEFINES): 1 drops the input DMAs after
+// the first K step, 2 the weight DMAs after the first, 4 the register split (the fp32 bits reused as the three terms)
+#ifndef SMC_X3_PROBE
+#define SMC_X3_PROBE 0
+#endif
 
 template <int WO, int WM, int TO, int TM, int BKT, int NST = SMC_X3_NST, int TAG = 0>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
@@ -769,7 +774,7 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
         char* st = smem + slot * STAGE;
         float* xs = reinterpret_cast<float*>(st + WB);
 #pragma unroll
-        for (int j = 0; j < XI; ++j) {
+        for (int j = 0; j < ((SMC_X3_PROBE & 1) && ks > ks_begin ? 0 : XI); ++j) {
             const int row = r0 + RSTEP * j;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 xrsrc, (__attribute__((address_space(3))) void*)(xs + row * BM + cw * 64), 4, voff,
@@ -779,7 +784,7 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
         // in global memory at (((t * cin / 16 + chunk) * 6 + run) * cout + o0 + o) * 8 bf16)
         const int64_t wbase = ((int64_t)t * c16n + ci0 / 16) * 6;
 #pragma unroll
-        for (int jw = 0; jw < WIW; ++jw) {
+        for (int jw = 0; jw < ((SMC_X3_PROBE & 2) && ks > ks_begin ? 0 : WIW); ++jw) {
             int j = wave + 4 * jw;
             if (j >= WLI) j -= WLI;  // wave-uniform
             const int L = j * 64 + lane;
@@ -835,7 +840,14 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
                 float xv[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) xv[e] = xcol[(kc * 16 + 8 * kh + e) * BM + j * 32];
-                x3_split8(xv, bt[j]);
+                if constexpr ((SMC_X3_PROBE & 4) != 0) {
+                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 w = {__float_as_uint(xv[0]), __float_as_uint(xv[2]), __float_as_uint(xv[4]),
+                                     __float_as_uint(xv[6])};
+                    bt[j][0] = bt[j][1] = bt[j][2] = __builtin_bit_cast(bf16x8, w);
+                } else {
+                    x3_split8(xv, bt[j]);
+                }
             }
 #pragma unroll
             for (int i = 0; i < TO; ++i)

@@ -30,7 +30,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="", help="comma-separated name filters, e.g. fwd_conv0 or fwd_conv0:128")
+    ap.add_argument("--fp32", action="store_true", help="exact-fp32 MFMA products (modconv.X3 = False)")
     args = ap.parse_args()
+    modconv.X3 = not args.fp32
     only = [f for f in args.only.split(",") if f]
     build.build(verbose=False)
     dev = "cuda"
