@@ -69,6 +69,14 @@ def adj_weight(W, ky, kx, in_scale=None, out_scale=None):
     return w
 
 
+# Split-bf16 products for the executor's direct GEMMs (include/stylemc_hip.h smc_conv_phase.wk_x3).  Off: the IR-SE50
+# input gradient of these seeded weights is ill-conditioned (PReLU kinks: the fp32 CPU path itself is 6.4e-3 of the max
+# away from fp64 at 4 / 8 faces), and the split products move which kinks flip -- x3 1e-6 / 3e-3 / 6e-3 against fp32
+# 1e-4 / 8e-5 / 9e-7 at 4 / 1 / 8 faces, cosine >= 0.9999994 either way (profiles/r04/irse_x3_diag.txt) -- for a
+# 0.1 ms / step kernel-time gain.  The reference-pinned tolerances stay those of the exact-fp32 products.
+X3 = False
+
+
 class _Packed:
     """Device tensors + ctypes descriptors of one IR-SE50 (kept alive together)."""
 
@@ -86,8 +94,8 @@ class _Packed:
 
         def phase(taps, stride, oh, ow, wk, oy=0, ox=0, sy=1, sx=1):
             wk = d(wk)
-            # split-bf16 planes for the direct GEMMs (modconv.X3; kept alive with the packed weights)
-            wx = modconv.x3_planes(wk, wk.shape[1], wk.shape[2])
+            # split-bf16 planes for the direct GEMMs (X3 below; kept alive with the packed weights)
+            wx = modconv.x3_planes(wk, wk.shape[1], wk.shape[2]) if X3 else None
             if wx is not None:
                 self.keep.append(wx)
             return _phase(taps, stride, oh, ow, oy, ox, sy, sx, wk, wx)
