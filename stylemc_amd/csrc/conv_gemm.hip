@@ -832,39 +832,65 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
         const short* Wp = reinterpret_cast<const short*>(st);
         const float* Xs = reinterpret_cast<const float*>(st + WB);
         const float* xcol = Xs + wm * TM * 32 + l32;
+        // Chunk pipeline: chunk kc + 1's fragment reads and input split are issued in the same region as chunk kc's
+        // MFMAs (no scheduling fence between them), so the LDS latency and the split VALU fill the MFMA issue gaps.
+        float xv[2][TM][8];
+        bf16x8 at[2][TO][3];
+        auto read_frags = [&](int kc, int b) {
 #pragma unroll
-        for (int kc = 0; kc < NKC; ++kc) {
-            bf16x8 bt[TM][3], at[TO][3];
+            for (int j = 0; j < TM; ++j)
 #pragma unroll
-            for (int j = 0; j < TM; ++j) {
-                float xv[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) xv[e] = xcol[(kc * 16 + 8 * kh + e) * BM + j * 32];
-                if constexpr ((SMC_X3_PROBE & 4) != 0) {
-                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-                    const u32x4 w = {__float_as_uint(xv[0]), __float_as_uint(xv[2]), __float_as_uint(xv[4]),
-                                     __float_as_uint(xv[6])};
-                    bt[j][0] = bt[j][1] = bt[j][2] = __builtin_bit_cast(bf16x8, w);
-                } else {
-                    x3_split8(xv, bt[j]);
-                }
-            }
+                for (int e = 0; e < 8; ++e) xv[b][j][e] = xcol[(kc * 16 + 8 * kh + e) * BM + j * 32];
 #pragma unroll
             for (int i = 0; i < TO; ++i)
 #pragma unroll
                 for (int s = 0; s < 3; ++s)
-                    at[i][s] = *reinterpret_cast<const bf16x8*>(
+                    at[b][i][s] = *reinterpret_cast<const bf16x8*>(
                         Wp + ((((kc * 3 + s) * 2 + kh) * BO) + wo * TO * 32 + i * 32 + l32) * 8);
-            __builtin_amdgcn_sched_barrier(0);
-            if (kc == 0 && issued < ks_end) {  // a later step's DMAs under this step's MFMAs
-                issue(issued, (issued - ks_begin) % NST);
-                ++issued;
+        };
+        read_frags(0, 0);
+        if (issued < ks_end) {  // a later step's DMAs, issued while this step's first reads are in flight
+            issue(issued, (issued - ks_begin) % NST);
+            ++issued;
+        }
+        bf16x8 bt[TM][3];
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+            if constexpr ((SMC_X3_PROBE & 4) != 0) {
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 w = {__float_as_uint(xv[0][j][0]), __float_as_uint(xv[0][j][2]),
+                                 __float_as_uint(xv[0][j][4]), __float_as_uint(xv[0][j][6])};
+                bt[j][0] = bt[j][1] = bt[j][2] = __builtin_bit_cast(bf16x8, w);
+            } else {
+                x3_split8(xv[0][j], bt[j]);
             }
+        }
+#pragma unroll
+        for (int kc = 0; kc < NKC; ++kc) {
+            const int b = kc & 1;
+            if (kc + 1 < NKC) read_frags(kc + 1, b ^ 1);
+            bf16x8 btn[TM][3];
 #pragma unroll
             for (int i = 0; i < TO; ++i)
 #pragma unroll
-                for (int j = 0; j < TM; ++j) acc[i][j] = x3_mma(at[i], bt[j], acc[i][j]);
-            __builtin_amdgcn_sched_barrier(0);
+                for (int j = 0; j < TM; ++j) acc[i][j] = x3_mma(at[b][i], bt[j], acc[i][j]);
+            if (kc + 1 < NKC) {
+#pragma unroll
+                for (int j = 0; j < TM; ++j) {
+                    if constexpr ((SMC_X3_PROBE & 4) != 0) {
+                        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                        const u32x4 w = {__float_as_uint(xv[b ^ 1][j][0]), __float_as_uint(xv[b ^ 1][j][2]),
+                                         __float_as_uint(xv[b ^ 1][j][4]), __float_as_uint(xv[b ^ 1][j][6])};
+                        btn[j][0] = btn[j][1] = btn[j][2] = __builtin_bit_cast(bf16x8, w);
+                    } else {
+                        x3_split8(xv[b ^ 1][j], btn[j]);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < TM; ++j)
+#pragma unroll
+                    for (int s = 0; s < 3; ++s) bt[j][s] = btn[j][s];
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragment reads of this slot done before the next barrier
     }
@@ -2102,7 +2128,9 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         grid.y = 1;
         RowTaps rt{};
         if (x3) {
-            const bool k32 = cfg == 0 && lds_bk32(cfg, cin);
+            // 32-channel K steps wherever the channels allow (two 16-channel chunks per barrier, the second's reads and
+            // split under the first's MFMAs)
+            const bool k32 = cfg == 0 && cin % 32 == 0;
             // 32-channel K steps for the narrow tiles too (A/B knob SMC_X3_K32_SMALL: half the barriers per FLOP)
             const bool k32s = SMC_X3_K32_SMALL && cin % 32 == 0;
             if (cfg == 0 && k32 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
