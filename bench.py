@@ -91,6 +91,8 @@ def parse():
                         "fp32-class error), fp32 = the exact-fp32 MFMA (modconv.X3)")
     p.add_argument("--vit-products", default="fp32", choices=["x3", "fp32"],
                    help="CLIP ViT projections: split-bf16 (x3) or exact-fp32 MFMA GEMMs (vit_hip.X3)")
+    p.add_argument("--irse-products", default=None, choices=["x3", "fp32"],
+                   help="IR-SE50 executor GEMMs: split-bf16 or exact-fp32 (irse_hip.X3; default: the library's)")
     p.add_argument("--schedule", default="prefetch", choices=["pair", "prefetch"],
                    help="stream schedule: pair = original synthesis beside the edited one; prefetch = the next "
                         "iteration's original synthesis on a third stream (DESIGN.md section 6b)")
@@ -328,6 +330,9 @@ def main():
     modconv.X3 = args.conv_products == "x3"
     from stylemc_amd import vit_hip
     vit_hip.X3 = args.vit_products == "x3"
+    from stylemc_amd import irse_hip
+    if args.irse_products is not None:
+        irse_hip.X3 = args.irse_products == "x3"
 
     G = load_generator("synthetic", args.resolution, dev)
     # weak scaling: 129 seeds per GPU and a global batch of 4 per GPU give every N the single-GPU schedule
@@ -459,6 +464,7 @@ def main():
                    "parallelism": f"dp{world.world_size}", "clip_type": args.clip_type, "clip_impl": args.clip_impl, "id_impl": args.id_impl,
                    "batched_loss_pairs": finder.batch_losses, "landmarks_loss_coef": 0,
                    "conv_products": args.conv_products, "vit_products": args.vit_products,
+                   "irse_products": "x3" if irse_hip.X3 else "fp32",
                    "direction_finite": finite, "world_size": world.world_size, "backend": world.backend,
                    "launcher": (os.environ.get("SMC_BENCH_LAUNCHER", "torch.distributed.run")
                                 if world.world_size > 1 else None),

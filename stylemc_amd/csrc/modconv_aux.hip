@@ -335,7 +335,27 @@ __global__ __launch_bounds__(256) void blur_act_fast(const float* t, int nsplit,
 // [ox0 - 4, ox0 + kFW + 4): a third of the load instructions of the scalar form, every one a full 16 B; the groups'
 // elements outside the tile window, the image width or the row are dropped / zeroed on the way into LDS.
 // Needs a 16-B aligned t, split_stride % 4 == 0, padx0 <= 4 and FW - 1 - padx0 <= 4.
-template <int FH, int FW>
+#ifndef SMC_BLUR_TPB
+#define SMC_BLUR_TPB 4
+#endif
+#ifndef SMC_BLUR_NT
+#define SMC_BLUR_NT 1
+#endif
+template <bool NT>
+__device__ __forceinline__ void st_f2(float* p, float2 v) {
+    if (NT) {
+        __builtin_nontemporal_store(v.x, p);
+        __builtin_nontemporal_store(v.y, p + 1);
+    } else {
+        *reinterpret_cast<float2*>(p) = v;
+    }
+}
+
+// TPB: row tiles per workgroup (grid.y = ceil(row tiles / TPB)), NT: non-temporal y / u stores (nothing reads y / u
+// before the next layer's conv has streamed the whole plane set).  Measured (profiles/r04/blur_ab/, bit-identical y):
+// TPB 4 + NT 712 -> 650 us over the five conv0 layers; TPB 8 / 16 no better; the same on the backward lost (dT is read
+// right away by the transposed conv's data gradient).
+template <int FH, int FW, int TPB, bool NT>
 __global__ __launch_bounds__(256) void blur_act_v4(const float* t, int nsplit, int64_t split_stride, float* y, int c,
                                                    int t_h, int t_w, int tp_w, int y_h, int y_w, const float* f,
                                                    int padx0, int pady0, float fgain, int flip, Epi e) {
@@ -344,95 +364,100 @@ __global__ __launch_bounds__(256) void blur_act_v4(const float* t, int nsplit, i
     constexpr int NL = (ROWS * G4 + 255) / 256;
     __shared__ float tile[ROWS * STRIDE];
     const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
-    const int ox0 = blockIdx.x * kFW, oy0 = blockIdx.y * kFH;  // fir_grid_fwd
+    const int ox0 = blockIdx.x * kFW;
     const int64_t nc = blockIdx.z;
     const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
     float tp[FH][FW];
     load_taps<FH, FW>(f, flip, fgain, tp);
-    const int iy0 = oy0 - pady0, ix0 = ox0 - padx0;
-    const int64_t pbase = nc * (int64_t)t_h * tp_w;
-    float4 v[NL];
-    int64_t off[NL];   // buffer index of the group's first element, -1: no valid element
-    int gx[NL];        // image column of the group's first element
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-        const int i = tid + 256 * l;
-        const int r = i / G4, q = i - r * G4;
-        const int iy = iy0 + r;
-        const int64_t row = pbase + (int64_t)iy * tp_w;
-        const int64_t g0 = ((row + ox0 - 4) & ~(int64_t)3) + 4 * q;
-        gx[l] = (int)(g0 - row);
-        const bool ok = i < ROWS * G4 && iy >= 0 && iy < t_h && gx[l] + 3 >= 0 && gx[l] < t_w;
-        off[l] = ok ? g0 : -1;
-        v[l] = *reinterpret_cast<const float4*>(t + (ok ? g0 : 0));
-    }
-    for (int s = 1; s < nsplit; ++s) {
-        const float* sp = t + s * split_stride;
-#pragma unroll
-        for (int l = 0; l < NL; ++l) {
-            const float4 a = *reinterpret_cast<const float4*>(sp + (off[l] >= 0 ? off[l] : 0));
-            v[l].x += a.x; v[l].y += a.y; v[l].z += a.z; v[l].w += a.w;
-        }
-    }
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-        const int i = tid + 256 * l;
-        if (i >= ROWS * G4) continue;
-        const int r = i / G4;
-        const float a[4] = {v[l].x, v[l].y, v[l].z, v[l].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int ix = gx[l] + k;
-            const int cc = ix - ix0;
-            if (cc >= 0 && cc < COLS) tile[r * STRIDE + cc] = (off[l] >= 0 && ix >= 0 && ix < t_w) ? a[k] : 0.f;
-        }
-    }
-    __syncthreads();
-    float out[4][2];
-    fir_block<FH, FW>(tile, STRIDE, 4 * ty, 2 * tx, tp, out);
     const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
     const float dv = e.d ? e.d[nc] : 1.f;
     const float bv = e.bias ? e.bias[o] : 0.f;
-    const int64_t plane = nc * (int64_t)y_h * y_w;
-    const int ox = ox0 + 2 * tx;
-    if (ox >= y_w) return;
-    // the 4 rows' noise is loaded before the first store (loaded next to each store, every row would wait for the
-    // previous row's stores: vmcnt counts both)
-    float2 nz[4];
+    for (int tb = 0; tb < TPB; ++tb) {
+        const int oy0 = (blockIdx.y * TPB + tb) * kFH;
+        if (oy0 >= y_h) break;
+        if (tb > 0) __syncthreads();  // the previous tile's FIR reads are done
+        const int iy0 = oy0 - pady0, ix0 = ox0 - padx0;
+        const int64_t pbase = nc * (int64_t)t_h * tp_w;
+        float4 v[NL];
+        int64_t off[NL];   // buffer index of the group's first element, -1: no valid element
+        int gx[NL];        // image column of the group's first element
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int oy = min(oy0 + 4 * ty + i, y_h - 1);
-        nz[i] = make_float2(0.f, 0.f);
-        if (e.mode != SMC_EPI_STORE && e.noise) {
-            nz[i] = *reinterpret_cast<const float2*>(e.noise + n * e.noise_nstride + (int64_t)oy * y_w + ox);
-            nz[i].x *= nstr;
-            nz[i].y *= nstr;
+        for (int l = 0; l < NL; ++l) {
+            const int i = tid + 256 * l;
+            const int r = i / G4, q = i - r * G4;
+            const int iy = iy0 + r;
+            const int64_t row = pbase + (int64_t)iy * tp_w;
+            const int64_t g0 = ((row + ox0 - 4) & ~(int64_t)3) + 4 * q;
+            gx[l] = (int)(g0 - row);
+            const bool ok = i < ROWS * G4 && iy >= 0 && iy < t_h && gx[l] + 3 >= 0 && gx[l] < t_w;
+            off[l] = ok ? g0 : -1;
+            v[l] = *reinterpret_cast<const float4*>(t + (ok ? g0 : 0));
         }
-    }
-    // the synthesis' conv0 epilogue (lrelu with 0 <= alpha <= 1, gain, clamp >= 0) with the activation fixed at
-    // compile time: max / min forms, bit-identical to smc::epi_y for finite values
-    const bool lrelu_clamp = e.act == SMC_ACT_LRELU && e.alpha >= 0.f && e.alpha <= 1.f && e.clamp >= 0.f;
+        for (int s = 1; s < nsplit; ++s) {
+            const float* sp = t + s * split_stride;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int oy = oy0 + 4 * ty + i;
-        if (oy >= y_h) continue;
-        const int64_t pix = (int64_t)oy * y_w + ox;
-        const float2 u2 = make_float2(out[i][0], out[i][1]);
-        if (e.mode == SMC_EPI_STORE) {
-            *reinterpret_cast<float2*>(y + plane + pix) = u2;
-            continue;
+            for (int l = 0; l < NL; ++l) {
+                const float4 a = *reinterpret_cast<const float4*>(sp + (off[l] >= 0 ? off[l] : 0));
+                v[l].x += a.x; v[l].y += a.y; v[l].z += a.z; v[l].w += a.w;
+            }
         }
-        if (e.u_save) *reinterpret_cast<float2*>(e.u_save + plane + pix) = u2;
-        float2 q;
-        if (lrelu_clamp) {
-            const float zx = __fmaf_rn(u2.x, dv, nz[i].x) + bv, zy = __fmaf_rn(u2.y, dv, nz[i].y) + bv;
-            q.x = fmaxf(fminf(fmaxf(zx, zx * e.alpha) * e.gain, e.clamp), -e.clamp);
-            q.y = fmaxf(fminf(fmaxf(zy, zy * e.alpha) * e.gain, e.clamp), -e.clamp);
-        } else {
-            q = make_float2(smc::epi_y(u2.x, dv, nz[i].x, bv, e.act, e.alpha, e.gain, e.clamp),
-                            smc::epi_y(u2.y, dv, nz[i].y, bv, e.act, e.alpha, e.gain, e.clamp));
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            const int i = tid + 256 * l;
+            if (i >= ROWS * G4) continue;
+            const int r = i / G4;
+            const float a[4] = {v[l].x, v[l].y, v[l].z, v[l].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int ix = gx[l] + k;
+                const int cc = ix - ix0;
+                if (cc >= 0 && cc < COLS) tile[r * STRIDE + cc] = (off[l] >= 0 && ix >= 0 && ix < t_w) ? a[k] : 0.f;
+            }
         }
-        *reinterpret_cast<float2*>(y + plane + pix) = q;
+        __syncthreads();
+        float out[4][2];
+        fir_block<FH, FW>(tile, STRIDE, 4 * ty, 2 * tx, tp, out);
+        const int64_t plane = nc * (int64_t)y_h * y_w;
+        const int ox = ox0 + 2 * tx;
+        if (ox >= y_w) continue;
+        // the 4 rows' noise is loaded before the first store (loaded next to each store, every row would wait for the
+        // previous row's stores: vmcnt counts both)
+        float2 nz[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int oy = min(oy0 + 4 * ty + i, y_h - 1);
+            nz[i] = make_float2(0.f, 0.f);
+            if (e.mode != SMC_EPI_STORE && e.noise) {
+                nz[i] = *reinterpret_cast<const float2*>(e.noise + n * e.noise_nstride + (int64_t)oy * y_w + ox);
+                nz[i].x *= nstr;
+                nz[i].y *= nstr;
+            }
+        }
+        // the synthesis' conv0 epilogue (lrelu with 0 <= alpha <= 1, gain, clamp >= 0) with the activation fixed at
+        // compile time: max / min forms, bit-identical to smc::epi_y for finite values
+        const bool lrelu_clamp = e.act == SMC_ACT_LRELU && e.alpha >= 0.f && e.alpha <= 1.f && e.clamp >= 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int oy = oy0 + 4 * ty + i;
+            if (oy >= y_h) continue;
+            const int64_t pix = (int64_t)oy * y_w + ox;
+            const float2 u2 = make_float2(out[i][0], out[i][1]);
+            if (e.mode == SMC_EPI_STORE) {
+                st_f2<NT>(y + plane + pix, u2);
+                continue;
+            }
+            if (e.u_save) st_f2<NT>(e.u_save + plane + pix, u2);
+            float2 q;
+            if (lrelu_clamp) {
+                const float zx = __fmaf_rn(u2.x, dv, nz[i].x) + bv, zy = __fmaf_rn(u2.y, dv, nz[i].y) + bv;
+                q.x = fmaxf(fminf(fmaxf(zx, zx * e.alpha) * e.gain, e.clamp), -e.clamp);
+                q.y = fmaxf(fminf(fmaxf(zy, zy * e.alpha) * e.gain, e.clamp), -e.clamp);
+            } else {
+                q = make_float2(smc::epi_y(u2.x, dv, nz[i].x, bv, e.act, e.alpha, e.gain, e.clamp),
+                                smc::epi_y(u2.y, dv, nz[i].y, bv, e.act, e.alpha, e.gain, e.clamp));
+            }
+            st_f2<NT>(y + plane + pix, q);
+        }
     }
 }
 
@@ -891,16 +916,18 @@ SMC_API int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_s
     SMC_CHECK((int64_t)n * c < 65536, "smc_modconv_blur_act_f32: too many planes");
     hipStream_t st = smc::as_stream(stream);
     if (fh == 4 && fw == 4) {
-        const dim3 grid = fir_grid_fwd((int64_t)n * c, y_w, y_h);
+        dim3 grid = fir_grid_fwd((int64_t)n * c, y_w, y_h);
         const uintptr_t al = (uintptr_t)t | (uintptr_t)y | (uintptr_t)epi->u_save | (uintptr_t)epi->noise;
         const bool v4 = split_stride % 4 == 0 && (al & 15) == 0 && y_w % 2 == 0 &&
                         epi->noise_nstride % 2 == 0 && padx0 <= 4 && fw - 1 - padx0 <= 4;
-        if (v4)
-            hipLaunchKernelGGL((blur_act_v4<4, 4>), grid, dim3(256), 0, st, t, nsplit, split_stride, y, c, t_h, t_w, tp_w,
+        if (v4) {
+            grid.y = (unsigned)smc::ceil_div((int)grid.y, SMC_BLUR_TPB);
+            hipLaunchKernelGGL((blur_act_v4<4, 4, SMC_BLUR_TPB, SMC_BLUR_NT != 0>), grid, dim3(256), 0, st, t, nsplit, split_stride, y, c, t_h, t_w, tp_w,
                                y_h, y_w, f, padx0, pady0, fgain, flip, to_epi(epi));
-        else
+        } else {
             hipLaunchKernelGGL((blur_act_fast<4, 4>), grid, dim3(256), 0, st, t, nsplit, split_stride, y, c, t_h, t_w,
                                tp_w, y_h, y_w, f, padx0, pady0, fgain, flip, to_epi(epi));
+        }
         return smc::check_launch("smc_modconv_blur_act_f32");
     }
     dim3 grid((unsigned)smc::ceil_div(y_w, kBT), (unsigned)smc::ceil_div(y_h, kBT), (unsigned)(n * c));

@@ -255,12 +255,25 @@ int lin_validate(const float* a, int lda, const float* b, int ldb, const float* 
 // one L2.
 constexpr int L2M = 32, L2N = 64, L2K = 64;
 
-__global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, int ntl) {
+#ifndef SMC_LIN_NST
+#define SMC_LIN_NST 2
+#endif
+#ifndef SMC_LIN_KW
+#define SMC_LIN_KW 2
+#endif
+// KW = 2: two wave quads per workgroup split each staged K step between them (k 0..31 / 32..63) and add their
+// accumulators through LDS at the end -- twice the waves per SIMD for the same tile grid and global traffic.
+// Measured (profiles/r04/lin_ab/, tools/bench_linear.py): the eight B = 4 projections 144.0 -> 134.8 us, B = 8
+// unchanged; NST = 3 (two steps in flight) 2-3 % slower at both batches.
+template <int NST, int KW>
+__global__ __launch_bounds__(256 * KW, 2) void lin_gemm2_kernel(LinParams p, int mt, int ntl) {
     constexpr int ATILE = L2M * L2K, BTILE = L2K * L2N, STAGE = ATILE + BTILE;
-    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+    constexpr int AJ = 2 / KW, BJ = 4 / KW, DW = AJ + BJ;  // DMAs per wave: A, B, per step
+    __shared__ __attribute__((aligned(16))) float smem[NST * STAGE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wq = wave & 3, kg = wave >> 2;
+    const int wm = wq >> 1, wn = wq & 1;
     // XCD-aware tile order (bijective for any grid size)
     const int nb = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
@@ -278,10 +291,10 @@ __global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, 
         float* As = smem + slot * STAGE;
         float* Bs = As + ATILE;
         const int k0 = ks * L2K;
-        // A: 512 float4 slots = 8 DMAs, 2 per wave; slot v -> row v/16, physical column v%16
+        // A: 512 float4 slots = 8 DMAs, AJ per wave; slot v -> row v/16, physical column v%16
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int base = (wave * 2 + j) * 256;           // float offset of this DMA in the tile
+        for (int j = 0; j < AJ; ++j) {
+            const int base = (wave * AJ + j) * 256;          // float offset of this DMA in the tile
             const int v = base / 4 + lane;
             const int row = v >> 4, cphys = v & 15;
             const int c = cphys ^ (row & 15);
@@ -289,10 +302,10 @@ __global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, 
             __builtin_amdgcn_global_load_lds((const void*)(p.a + (int64_t)grow * p.lda + k0 + 4 * c),
                                              (__attribute__((address_space(3))) void*)(As + base), 16, 0, 0);
         }
-        // B: 1024 float4 slots = 16 DMAs, 4 per wave; slot v -> k-row v/16, physical column v%16
+        // B: 1024 float4 slots = 16 DMAs, BJ per wave; slot v -> k-row v/16, physical column v%16
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int base = (wave * 4 + j) * 256;
+        for (int j = 0; j < BJ; ++j) {
+            const int base = (wave * BJ + j) * 256;
             const int v = base / 4 + lane;
             const int krow = v >> 4, cphys = v & 15;
             const int c = cphys ^ (((krow >> 2) & 1) << 2);
@@ -305,16 +318,25 @@ __global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, 
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const int i = lane & 15, g = lane >> 4;  // A row / B column within the block, k group
     const int arow = wm * 16 + i;
-    if (ks0 < ks1) issue(ks0, 0);
+    // NST-stage ring: NST - 1 steps in flight ahead of the one being multiplied (DW DMAs per wave per step)
+#pragma unroll
+    for (int j = 0; j < NST - 1; ++j)
+        if (ks0 + j < ks1) issue(ks0 + j, j);
     for (int ks = ks0; ks < ks1; ++ks) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int ahead = min(NST - 2, ks1 - 1 - ks);  // later steps that may stay in flight
+        if (NST >= 4 && ahead >= 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DW) : "memory");
+        else if (NST >= 3 && ahead >= 1)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DW) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (ks + 1 < ks1) issue(ks + 1, (ks + 1 - ks0) & 1);
-        const float* As = smem + ((ks - ks0) & 1) * STAGE;
+        if (ks + NST - 1 < ks1) issue(ks + NST - 1, (ks + NST - 1 - ks0) % NST);
+        const float* As = smem + ((ks - ks0) % NST) * STAGE;
         const float* Bs = As + ATILE;
 #pragma unroll
-        for (int kc = 0; kc < L2K; kc += 16) {
+        for (int kc = kg * (L2K / KW); kc < (kg + 1) * (L2K / KW); kc += 16) {
             // A: row arow, k = kc + 4g .. +3 -> logical float4 column (kc/4 + g)
             const int ca = (kc / 4 + g) ^ (arow & 15);
             const f32x4 av = *reinterpret_cast<const f32x4*>(As + arow * L2K + 4 * ca);
@@ -337,6 +359,24 @@ __global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, 
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    if (KW == 2) {  // the second quad's partial sums through LDS (every wave is past its last LDS read)
+        __syncthreads();
+        float* red = smem + wq * 512 + lane;
+        if (kg == 1) {
+#pragma unroll
+            for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) red[(blk * 4 + rr) * 64] = acc[blk][rr];
+        }
+        __syncthreads();
+        if (kg == 0) {
+#pragma unroll
+            for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) acc[blk][rr] += red[(blk * 4 + rr) * 64];
+        }
+    }
+    const bool writer = kg == 0;
     // epilogue: block blk, register rr -> row 4g + rr, column i
 #pragma unroll
     for (int blk = 0; blk < 2; ++blk) {
@@ -344,7 +384,7 @@ __global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, 
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
             const int m = m0 + wm * 16 + 4 * g + rr;
-            if (m >= p.M) continue;
+            if (m >= p.M || !writer) continue;
             if (p.nsplit == 1)
                 p.c[(int64_t)m * p.ldc + n] = lin_epi(acc[blk][rr], m, n, p.e);
             else if (p.counters)  // write-through (sc1): the hand-off below needs no release fence
@@ -374,7 +414,7 @@ __global__ __launch_bounds__(256, 2) void lin_gemm2_kernel(LinParams p, int mt, 
         *flag = last;
     }
     __syncthreads();
-    if (!*flag) return;
+    if (!*flag || !writer) return;
     // split-major sums: all 8 loads of one split in flight before the adds; rows past M re-read row M - 1
     float v[2][4];
     for (int k = 0; k < p.nsplit; ++k) {
@@ -649,7 +689,8 @@ int lin_launch(const float* a, int lda, const float* b, int ldb, float* c, int l
         hipLaunchKernelGGL(lin_gemm2_x3_kernel, dim3((unsigned)(mt * ntl * p.nsplit)), dim3(256), 0, st, p, bx3, mt, ntl);
     } else if (v2) {
         const int mt = (int)smc::ceil_div(M, L2M), ntl = N / L2N;
-        hipLaunchKernelGGL(lin_gemm2_kernel, dim3((unsigned)(mt * ntl * p.nsplit)), dim3(256), 0, st, p, mt, ntl);
+        hipLaunchKernelGGL((lin_gemm2_kernel<SMC_LIN_NST, SMC_LIN_KW>), dim3((unsigned)(mt * ntl * p.nsplit)),
+                           dim3(256 * SMC_LIN_KW), 0, st, p, mt, ntl);
     } else {
         dim3 grid((unsigned)smc::ceil_div(M, LBM), (unsigned)smc::ceil_div(N, LBN), (unsigned)p.nsplit);
         hipLaunchKernelGGL(lin_gemm_kernel, grid, dim3(LNT), 0, st, p);
