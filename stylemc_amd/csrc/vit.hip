@@ -265,7 +265,11 @@ constexpr int L2M = 32, L2N = 64, L2K = 64;
 // accumulators through LDS at the end -- twice the waves per SIMD for the same tile grid and global traffic.
 // Measured (profiles/r04/lin_ab/, tools/bench_linear.py): the eight B = 4 projections 144.0 -> 134.8 us, B = 8
 // unchanged; NST = 3 (two steps in flight) 2-3 % slower at both batches.
-template <int NST, int KW>
+// BT: B given transposed, bt [N][K] row-major (ldb = its row pitch): the B tile is staged like the A tile (k fastest,
+// XOR-swizzled float4 columns) and a B fragment (4 consecutive k of one column) is one ds_read_b128 instead of four
+// ds_read_b32.  Every ViT projection has both orientations in the packed buffer (W^T for the forward, W for the
+// data gradient), so the executor hands each call the other one.
+template <int NST, int KW, bool BT>
 __global__ __launch_bounds__(256 * KW, 2) void lin_gemm2_kernel(LinParams p, int mt, int ntl) {
     constexpr int ATILE = L2M * L2K, BTILE = L2K * L2N, STAGE = ATILE + BTILE;
     constexpr int AJ = 2 / KW, BJ = 4 / KW, DW = AJ + BJ;  // DMAs per wave: A, B, per step
@@ -303,14 +307,20 @@ __global__ __launch_bounds__(256 * KW, 2) void lin_gemm2_kernel(LinParams p, int
                                              (__attribute__((address_space(3))) void*)(As + base), 16, 0, 0);
         }
         // B: 1024 float4 slots = 16 DMAs, BJ per wave; slot v -> k-row v/16, physical column v%16
+        // (BT: n-row v/16 of bt, physical k-column v%16, swizzled as A)
 #pragma unroll
         for (int j = 0; j < BJ; ++j) {
             const int base = (wave * BJ + j) * 256;
             const int v = base / 4 + lane;
-            const int krow = v >> 4, cphys = v & 15;
-            const int c = cphys ^ (((krow >> 2) & 1) << 2);
-            __builtin_amdgcn_global_load_lds((const void*)(p.b + (int64_t)(k0 + krow) * p.ldb + n0 + 4 * c),
-                                             (__attribute__((address_space(3))) void*)(Bs + base), 16, 0, 0);
+            const int row = v >> 4, cphys = v & 15;
+            const float* src;
+            if constexpr (BT) {
+                src = p.b + (int64_t)(n0 + row) * p.ldb + k0 + 4 * (cphys ^ (row & 15));
+            } else {
+                src = p.b + (int64_t)(k0 + row) * p.ldb + n0 + 4 * (cphys ^ (((row >> 2) & 1) << 2));
+            }
+            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(Bs + base),
+                                             16, 0, 0);
         }
     };
 
@@ -341,14 +351,24 @@ __global__ __launch_bounds__(256 * KW, 2) void lin_gemm2_kernel(LinParams p, int
             const int ca = (kc / 4 + g) ^ (arow & 15);
             const f32x4 av = *reinterpret_cast<const f32x4*>(As + arow * L2K + 4 * ca);
             float bv[2][4];
-#pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) {
-                const int krow = kc + 4 * g + s2;
-                const int sw = ((krow >> 2) & 1) << 2;
+            if constexpr (BT) {
 #pragma unroll
                 for (int blk = 0; blk < 2; ++blk) {
                     const int n = wn * 32 + blk * 16 + i;
-                    bv[blk][s2] = Bs[krow * L2N + 4 * ((n >> 2) ^ sw) + (n & 3)];
+                    const f32x4 b4 = *reinterpret_cast<const f32x4*>(Bs + n * L2K + 4 * ((kc / 4 + g) ^ (n & 15)));
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2) bv[blk][s2] = b4[s2];
+                }
+            } else {
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    const int krow = kc + 4 * g + s2;
+                    const int sw = ((krow >> 2) & 1) << 2;
+#pragma unroll
+                    for (int blk = 0; blk < 2; ++blk) {
+                        const int n = wn * 32 + blk * 16 + i;
+                        bv[blk][s2] = Bs[krow * L2N + 4 * ((n >> 2) ^ sw) + (n & 3)];
+                    }
                 }
             }
 #pragma unroll
@@ -667,9 +687,13 @@ int64_t lin_ws_floats(int M, int N, int K) {
     return s > 1 ? (int64_t)s * M * N : 0;
 }
 
+#ifndef SMC_LIN_BT
+#define SMC_LIN_BT 1
+#endif
+// bt (optional): the same B transposed, [N][K] row-major with row pitch K; used by the v2 kernel (SMC_LIN_BT)
 int lin_launch(const float* a, int lda, const float* b, int ldb, float* c, int ldc, int M, int N, int K,
                const smc_linear_epilogue* epi, float* ws, int64_t ws_bytes, hipStream_t st, int* counters = nullptr,
-               const short* bx3 = nullptr) {
+               const short* bx3 = nullptr, const float* bt = nullptr) {
     int rc = lin_validate(a, lda, b, ldb, c, ldc, M, N, K);
     if (rc != SMC_OK) return rc;
     LinParams p{};
@@ -689,8 +713,16 @@ int lin_launch(const float* a, int lda, const float* b, int ldb, float* c, int l
         hipLaunchKernelGGL(lin_gemm2_x3_kernel, dim3((unsigned)(mt * ntl * p.nsplit)), dim3(256), 0, st, p, bx3, mt, ntl);
     } else if (v2) {
         const int mt = (int)smc::ceil_div(M, L2M), ntl = N / L2N;
-        hipLaunchKernelGGL((lin_gemm2_kernel<SMC_LIN_NST, SMC_LIN_KW>), dim3((unsigned)(mt * ntl * p.nsplit)),
-                           dim3(256 * SMC_LIN_KW), 0, st, p, mt, ntl);
+        if (SMC_LIN_BT && bt && K % 4 == 0 && (reinterpret_cast<uintptr_t>(bt) & 15) == 0) {
+            LinParams q = p;
+            q.b = bt;
+            q.ldb = K;
+            hipLaunchKernelGGL((lin_gemm2_kernel<SMC_LIN_NST, SMC_LIN_KW, true>), dim3((unsigned)(mt * ntl * p.nsplit)),
+                               dim3(256 * SMC_LIN_KW), 0, st, q, mt, ntl);
+        } else {
+            hipLaunchKernelGGL((lin_gemm2_kernel<SMC_LIN_NST, SMC_LIN_KW, false>), dim3((unsigned)(mt * ntl * p.nsplit)),
+                               dim3(256 * SMC_LIN_KW), 0, st, p, mt, ntl);
+        }
     } else {
         dim3 grid((unsigned)smc::ceil_div(M, LBM), (unsigned)smc::ceil_div(N, LBN), (unsigned)p.nsplit);
         hipLaunchKernelGGL(lin_gemm_kernel, grid, dim3(LNT), 0, st, p);
@@ -1470,14 +1502,14 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
     const float eps = cfg->ln_eps;
     int64_t cursor = 0;
     auto lin = [&](const float* a, int lda, const float* bw, int ldb, float* c, int ldc, int MM, int N, int K,
-                   const smc_linear_epilogue& e, const short* bx3) {
+                   const smc_linear_epilogue& e, const short* bx3, const float* bt) {
         int* ctr = ws.counters + cursor;
         cursor += ws.counter_slice;
         if (cursor > ws.counter_ints) {
             smc::set_error("smc_vit: split-K counter slices exhausted");
             return SMC_ERR_INVALID;
         }
-        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr, bx3);
+        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr, bx3, bt);
     };
     if (hipMemsetAsync(ws.counters, 0, sizeof(int) * (size_t)ws.counter_ints, st) != hipSuccess) {
         smc::set_error("smc_vit: counter memset failed");
@@ -1486,7 +1518,7 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
 
     // patch embedding + class token + positional embedding, ln_pre
     SMC_TRY(smc_patch_im2col_f32(image, ws.patches, B, d.C, d.G, d.p, 0, stream));
-    SMC_TRY(lin(ws.patches, d.P, w.conv_wt, D, ws.tok, D, Mt, D, d.P, epi_none(), w.conv_wt3));
+    SMC_TRY(lin(ws.patches, d.P, w.conv_wt, D, ws.tok, D, Mt, D, d.P, epi_none(), w.conv_wt3, w.conv_w));
     float* x_pre = saved ? sv.x_pre : ws.xb;
     hipLaunchKernelGGL(embed_fwd_kernel, dim3(ew_blocks((int64_t)M * D)), dim3(256), 0, st, ws.tok, w.cls, w.pos,
                        x_pre, B, d.L, D);
@@ -1509,13 +1541,13 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
                               saved ? ls.rs1 : nullptr, M, D, eps, st));
         smc_linear_epilogue e = epi_none();
         e.bias = lw.qkv_b;
-        SMC_TRY(lin(ws.h, D, lw.qkv_wt, 3 * D, qkv, 3 * D, M, 3 * D, D, e, lw.qkv_wt3));
+        SMC_TRY(lin(ws.h, D, lw.qkv_wt, 3 * D, qkv, 3 * D, M, 3 * D, D, e, lw.qkv_wt3, lw.qkv_w));
         SMC_TRY(attn_fwd_launch(qkv, ws.o, saved ? ls.P : nullptr, B, d.L, d.H, scale, st));
         e = epi_none();
         e.bias = lw.out_b;
         e.residual = x_in;
         e.ld_res = D;
-        SMC_TRY(lin(ws.o, D, lw.out_wt, D, x_mid, D, M, D, D, e, lw.out_wt3));
+        SMC_TRY(lin(ws.o, D, lw.out_wt, D, x_mid, D, M, D, D, e, lw.out_wt3, lw.out_w));
         // MLP block: x_out = x_mid + c_proj(QuickGELU(c_fc(ln_2(x_mid))))
         SMC_TRY(ln_fwd_launch(x_mid, D, lw.ln2_w, lw.ln2_b, ws.h, D, saved ? ls.mu2 : nullptr,
                               saved ? ls.rs2 : nullptr, M, D, eps, st));
@@ -1524,18 +1556,18 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
         e.act = SMC_LIN_ACT_QUICKGELU;
         e.pre_save = saved ? ls.G : nullptr;
         e.ld_pre = 4 * D;
-        SMC_TRY(lin(ws.h, D, lw.fc_wt, 4 * D, ws.big, 4 * D, M, 4 * D, D, e, lw.fc_wt3));
+        SMC_TRY(lin(ws.h, D, lw.fc_wt, 4 * D, ws.big, 4 * D, M, 4 * D, D, e, lw.fc_wt3, lw.fc_w));
         e = epi_none();
         e.bias = lw.pr_b;
         e.residual = x_mid;
         e.ld_res = D;
-        SMC_TRY(lin(ws.big, 4 * D, lw.pr_wt, D, x_out, D, M, D, 4 * D, e, lw.pr_wt3));
+        SMC_TRY(lin(ws.big, 4 * D, lw.pr_wt, D, x_out, D, M, D, 4 * D, e, lw.pr_wt3, lw.pr_w));
         x = x_out;
     }
     // head: ln_post(x[:, 0]) @ proj   (CLS rows, stride L*D)
     SMC_TRY(ln_fwd_launch(x, (int64_t)d.L * D, w.lnpost_w, w.lnpost_b, ws.h, D, saved ? sv.mupost : nullptr,
                           saved ? sv.rspost : nullptr, B, D, eps, st));
-    return lin(ws.h, D, w.proj, d.E, out, d.E, B, d.E, D, epi_none(), w.proj3);
+    return lin(ws.h, D, w.proj, d.E, out, d.E, B, d.E, D, epi_none(), w.proj3, w.proj_t);
 }
 
 SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed, const float* dout, int batch,
@@ -1560,14 +1592,14 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
     saved_layout(d, batch, const_cast<float*>(saved), &sv);
     int64_t cursor = 0;
     auto lin = [&](const float* a, int lda, const float* bw, int ldb, float* c, int ldc, int MM, int N, int K,
-                   const smc_linear_epilogue& e, const short* bx3) {
+                   const smc_linear_epilogue& e, const short* bx3, const float* bt) {
         int* ctr = ws.counters + cursor;
         cursor += ws.counter_slice;
         if (cursor > ws.counter_ints) {
             smc::set_error("smc_vit: split-K counter slices exhausted");
             return SMC_ERR_INVALID;
         }
-        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr, bx3);
+        return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr, bx3, bt);
     };
     if (hipMemsetAsync(ws.counters, 0, sizeof(int) * (size_t)ws.counter_ints, st) != hipSuccess) {
         smc::set_error("smc_vit: counter memset failed");
@@ -1575,7 +1607,7 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
     }
 
     // head: d(ln_post out) = dout @ proj^T, then ln_post backward into the CLS rows of a zeroed dx
-    SMC_TRY(lin(dout, d.E, w.proj_t, D, ws.h, D, B, D, d.E, epi_none(), w.proj_t3));
+    SMC_TRY(lin(dout, d.E, w.proj_t, D, ws.h, D, B, D, d.E, epi_none(), w.proj_t3, w.proj));
     if (hipMemsetAsync(ws.dx, 0, sizeof(float) * (size_t)M * D, st) != hipSuccess) {
         smc::set_error("smc_vit_backward_f32: memset failed");
         return SMC_ERR_LAUNCH;
@@ -1592,19 +1624,19 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
         smc_linear_epilogue e = epi_none();
         e.dact_pre = ls.G;
         e.ld_dact = 4 * D;
-        SMC_TRY(lin(dx, D, lw.pr_w, 4 * D, ws.big, 4 * D, M, 4 * D, D, e, lw.pr_w3));   // dG = (dx @ W_proj) * gelu'(G)
-        SMC_TRY(lin(ws.big, 4 * D, lw.fc_w, D, ws.dh, D, M, D, 4 * D, epi_none(), lw.fc_w3));  // dh2 = dG @ W_fc
+        SMC_TRY(lin(dx, D, lw.pr_w, 4 * D, ws.big, 4 * D, M, 4 * D, D, e, lw.pr_w3, lw.pr_wt));   // dG = (dx @ W_proj) * gelu'(G)
+        SMC_TRY(lin(ws.big, 4 * D, lw.fc_w, D, ws.dh, D, M, D, 4 * D, epi_none(), lw.fc_w3, lw.fc_wt));  // dh2 = dG @ W_fc
         SMC_TRY(ln_bwd_launch(ws.dh, D, ls.x_mid, D, ls.mu2, ls.rs2, lw.ln2_w, dx, D, dx, D, M, D, st));
         // attention block
-        SMC_TRY(lin(dx, D, lw.out_w, D, ws.o, D, M, D, D, epi_none(), lw.out_w3));       // dO = dx_mid @ W_out
+        SMC_TRY(lin(dx, D, lw.out_w, D, ws.o, D, M, D, D, epi_none(), lw.out_w3, lw.out_wt));       // dO = dx_mid @ W_out
         SMC_TRY(attn_bwd_launch(ws.o, ls.qkv, ls.P, ws.qkv, B, d.L, d.H, scale, st));
-        SMC_TRY(lin(ws.qkv, 3 * D, lw.qkv_w, D, ws.dh, D, M, D, 3 * D, epi_none(), lw.qkv_w3));  // dh1 = dqkv @ W_in
+        SMC_TRY(lin(ws.qkv, 3 * D, lw.qkv_w, D, ws.dh, D, M, D, 3 * D, epi_none(), lw.qkv_w3, lw.qkv_wt));  // dh1 = dqkv @ W_in
         SMC_TRY(ln_bwd_launch(ws.dh, D, ls.x_in, D, ls.mu1, ls.rs1, lw.ln1_w, dx, D, dx, D, M, D, st));
     }
     // ln_pre backward, drop the class-token row, patch GEMM adjoint, col2im
     SMC_TRY(ln_bwd_launch(dx, D, sv.x_pre, D, sv.mu0, sv.rs0, w.lnpre_w, nullptr, 0, ws.dh, D, M, D, st));
     hipLaunchKernelGGL(embed_bwd_kernel, dim3(ew_blocks((int64_t)Mt * D)), dim3(256), 0, st, ws.dh, ws.tok, B, d.L, D);
     SMC_TRY(smc::check_launch("vit embed bwd"));
-    SMC_TRY(lin(ws.tok, D, w.conv_w, d.P, ws.patches, d.P, Mt, d.P, D, epi_none(), w.conv_w3));
+    SMC_TRY(lin(ws.tok, D, w.conv_w, d.P, ws.patches, d.P, Mt, d.P, D, epi_none(), w.conv_w3, w.conv_wt));
     return smc_patch_im2col_f32(dimage, ws.patches, B, d.C, d.G, d.p, 1, stream);
 }
