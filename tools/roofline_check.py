@@ -4,7 +4,8 @@ roofline pass) against the rocprofv3 kernel trace of the same run.
     python tools/roofline_check.py run_kernel_trace.csv [launches=100]
 
 The roofline pass is the last `launches` synthesis-GEMM calls of the run.  One smc_conv_gemm_f32 call is
-the GEMM kernel (TAG 0) plus, where the layer needs them, the per-sample weight kernel launched right before
+the GEMM kernel (TAG 0) plus, where the layer needs them, the per-sample weight kernel (wscale_kernel, or
+x3_weights_kernel for the split-bf16 planes) launched right before
 it (wscale_kernel) and the split-K reduction launched right after it (epilogue_kernel); the HIP events
 bracket all of them, so both the kernel-only and the whole-call averages are printed."""
 import csv
@@ -30,7 +31,7 @@ def main():
         j = i - 1
         while j >= 0 and rows[j]["Stream_Id"] != st:
             j -= 1
-        if j >= 0 and ("wscale_kernel" in rows[j]["Kernel_Name"] or "xscale_kernel" in rows[j]["Kernel_Name"]):
+        if j >= 0 and any(k in rows[j]["Kernel_Name"] for k in ("wscale_kernel", "xscale_kernel", "x3_weights_kernel")):
             start = int(rows[j]["Start_Timestamp"])
         j = i + 1
         while j < len(rows) and rows[j]["Stream_Id"] != st:
