@@ -61,14 +61,26 @@ struct WinoParams {
     float* ws;             // the partial planes [nsplit][n][cout][h][w]
 };
 
+// Staged row pitch: CHP >= CH 16-B chunks (the pad chunks are sentinel DMA lanes, zero-filled) so that a channel slab
+// is 32 floats mod 64.  A lane reads its 4 x 4 patch as three aligned 8-B reads per row (columns 2 tc + 2 .. + 7 of
+// the staged row); in a read group the 16 tiles' pairs of one channel cover 32 consecutive dwords and the other
+// channel's are one slab away, i.e. the other 32 of the 64 banks: conflict-free.  (Reads of the unaligned patch start
+// compile to ds_read2_b32 pairs at lane stride 2: two lanes on every bank, a third of the kernel's LDS cycles.)
+constexpr int wino_chp(int rows, int ch) {
+    int c = ch;
+    while ((rows * 4 * c) % 64 != 32) ++c;
+    return c;
+}
+
 template <int TC>
 struct WinoCfg {
     static constexpr int TR = WBT / TC;             // tile rows of the block
     static constexpr int ROWS = 2 * TR + 2;         // staged input rows
     static constexpr int CH = TC / 2 + 2;           // 16-B chunks per staged row (2 TC + 8 floats)
-    static constexpr int PITCH = 4 * CH;
-    static constexpr int SLAB = ROWS * PITCH;       // floats per channel
-    static constexpr int PL = WBK * ROWS * CH;      // DMA lanes of the patch
+    static constexpr int CHP = wino_chp(ROWS, CH);  // ... with the pad chunks
+    static constexpr int PITCH = 4 * CHP;
+    static constexpr int SLAB = ROWS * PITCH;       // floats per channel (32 mod 64)
+    static constexpr int PL = WBK * ROWS * CHP;     // DMA lanes of the patch (pad lanes included)
     static constexpr int PJ = (PL + 63) / 64;       // patch DMA wave-instructions per step
     static constexpr int PF = PJ * 256;             // floats reserved for the patch (whole instructions)
     static constexpr int UF = WBK * 16 * WBO;       // floats of the U slab
@@ -103,7 +115,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void wino_kernel(WinoParams p) {
     using C = WinoCfg<TC>;
     constexpr int OBW = 2, NW = C::NW, UJW = C::UJW, PJW = C::PJW;
-    constexpr int TR = C::TR, ROWS = C::ROWS, CH = C::CH, PITCH = C::PITCH, SLAB = C::SLAB, STAGE = C::STAGE;
+    constexpr int TR = C::TR, ROWS = C::ROWS, CH = C::CH, CHP = C::CHP, PITCH = C::PITCH, SLAB = C::SLAB;
+    constexpr int STAGE = C::STAGE;
     __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
     const int tid = threadIdx.x;
@@ -146,11 +159,11 @@ void wino_kernel(WinoParams p) {
 #pragma unroll
         for (int jj = 0; jj < PJW; ++jj) {
             const int L = (wave + NW * jj) * 64 + lane;
-            const int c = L / (ROWS * CH);
-            const int r2 = L - c * (ROWS * CH);
-            const int r = r2 / CH, ch = r2 - r * CH;
+            const int c = L / (ROWS * CHP);
+            const int r2 = L - c * (ROWS * CHP);
+            const int r = r2 / CHP, ch = r2 - r * CHP;
             const int gyy = 2 * it.ty0 - 1 + r, gxx = 2 * it.tx0 - 4 + 4 * ch;
-            const bool ok = c < WBK && gyy >= 0 && gyy < H && gxx >= 0 && gxx < W;
+            const bool ok = c < WBK && ch < CH && gyy >= 0 && gyy < H && gxx >= 0 && gxx < W;
             pv[jj] = ok ? (int)((((int64_t)(it.nn * p.cin + c) * H + gyy) * W + gxx) * 4) : 0x7ffffff0;
         }
     };
@@ -185,7 +198,7 @@ void wino_kernel(WinoParams p) {
     const int kq_lane = lane >> 4;   // MFMA k (channel within a k-quad)
     const int tl = 16 * wave + (lane & 15);
     const int tr = tl / TC, tc = tl - tr * TC;
-    const int poff = kq_lane * SLAB + 2 * tr * PITCH + 2 * tc + 3;
+    const int poff = kq_lane * SLAB + 2 * tr * PITCH + 2 * tc + 2;  // (even: 8-B aligned pairs; the patch starts at +1)
     const int uoff = (kq_lane * 4 * WBO + (lane & 15)) * 4;
     const bool has_s = SM == 1 ? true : SM == 2 ? false : p.s != nullptr;
 
@@ -208,10 +221,17 @@ void wino_kernel(WinoParams p) {
     auto load_patch = [&](const float* ps, int kq) {
         if constexpr ((PROBE & 32) != 0) return;
         const float* pp = ps + kq * 4 * SLAB + poff;
+        typedef float f32x2 __attribute__((ext_vector_type(2), aligned(8)));
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) pd[4 * i + j] = pp[i * PITCH + j];
+        for (int i = 0; i < 4; ++i) {
+            const f32x2 a = *reinterpret_cast<const f32x2*>(pp + i * PITCH);
+            const f32x2 b = *reinterpret_cast<const f32x2*>(pp + i * PITCH + 2);
+            const f32x2 c = *reinterpret_cast<const f32x2*>(pp + i * PITCH + 4);
+            pd[4 * i + 0] = a[1];
+            pd[4 * i + 1] = b[0];
+            pd[4 * i + 2] = b[1];
+            pd[4 * i + 3] = c[0];
+        }
     };
     auto load_a = [&](const float* us, int gi, f32x4 (&a)[OBW]) {
         if constexpr ((PROBE & 32) != 0) {
@@ -486,9 +506,14 @@ int wino_tc(int h, int w) {
 // One workgroup per work item.  (The persistent form -- PERSIST = 1, a resident grid looping over items with the
 // next item's first DMA under the current item's last step -- measured 3-18 % slower on every synthesis shape:
 // tools/probes/wino_ab.hip, profiles/r03_wino_ab.txt.)
+// (timing / counter probes only: tools/ builds a variant library with -DSMC_WINO_PROBE=n, see wino_kernel's PROBE)
+#ifndef SMC_WINO_PROBE
+#define SMC_WINO_PROBE 0
+#endif
 template <int TC, int SM, int EK>
 void launch_wino(const WinoParams& p, int64_t items, hipStream_t st) {
-    hipLaunchKernelGGL((wino_kernel<TC, SM, EK, 0>), dim3((unsigned)items, (unsigned)p.nsplit), dim3(256), 0, st, p);
+    hipLaunchKernelGGL((wino_kernel<TC, SM, EK, 0, SMC_WINO_PROBE>), dim3((unsigned)items, (unsigned)p.nsplit), dim3(256),
+                       0, st, p);
 }
 
 template <int SM, int EK>
