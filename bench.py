@@ -66,8 +66,8 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--resolution", type=int, default=1024)
     p.add_argument("--batch", type=int, default=4, help="seeds per GPU per step")
     p.add_argument("--n-seeds", type=int, default=None,
