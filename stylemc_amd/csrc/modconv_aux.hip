@@ -24,6 +24,7 @@ struct Epi {
     float* u_save;
     smc::EpiExt ext;
     int grad_from_y;
+    float* dd_part;  // set: the act / FIR backward kernels store their per-tile dd partials here (dd_sum_kernel adds them)
 };
 
 Epi to_epi(const smc_conv_epilogue* e) {
@@ -563,9 +564,12 @@ __global__ __launch_bounds__(256) void blur_act_bwd_fast(const float* g, const f
             if (ox < t_w) dt[tplane + (int64_t)oy * tp_w + ox] = out[i][j];
         }
     }
-    if (dd) {
+    if (dd || e.dd_part) {
         const float tot = block_sum256(part, red);
-        if (tid == 0) atomicAdd(dd + nc, tot);
+        if (tid == 0) {
+            if (e.dd_part) e.dd_part[nc * (gridDim.y * gridDim.z) + blockIdx.z * gridDim.y + blockIdx.y] = tot;
+            else atomicAdd(dd + nc, tot);
+        }
     }
 }
 
@@ -650,9 +654,12 @@ __global__ __launch_bounds__(256) void blur_act_bwd_v4(const float* g, const flo
             if (ox < t_w) dt[tplane + (int64_t)oy * tp_w + ox] = out[i][j];
         }
     }
-    if (dd) {
+    if (dd || e.dd_part) {
         const float tot = block_sum256(part, red);
-        if (tid == 0) atomicAdd(dd + nc, tot);
+        if (tid == 0) {
+            if (e.dd_part) e.dd_part[nc * (gridDim.y * gridDim.z) + blockIdx.z * gridDim.y + blockIdx.y] = tot;
+            else atomicAdd(dd + nc, tot);
+        }
     }
 }
 
@@ -700,48 +707,29 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const float* g, const floa
         du[base + p] = dz * dv;
         part += dz * uv;
     }
-    if (dd) {
+    if (dd || e.dd_part) {
         const float tot = block_sum256(part, red);
-        if (threadIdx.x == 0) atomicAdd(dd + nc, tot);
+        if (threadIdx.x == 0) {
+            if (e.dd_part) e.dd_part[nc * gridDim.x + blockIdx.x] = tot;
+            else atomicAdd(dd + nc, tot);
+        }
     }
 }
 
-// dd[n, o] += sum_hw dz * u with ONE workgroup per plane (fixed thread strides, fixed reduction tree): the style
-// gradient of the demodulation is then bit-reproducible whatever the plane size.  The fused act / FIR backward
-// kernels add their per-tile partials with float atomics, which is order-independent only while a plane has at most
-// two dd-owning tiles (two addends onto zero commute) -- true for every trainable layer of find_direction (b8..b64);
-// larger planes run those kernels without dd and this pass after them (dd_planes_need_pass).
-__global__ __launch_bounds__(256) void dd_plane_kernel(const float* g, const float* u, float* dd, int c, int64_t hw,
-                                                       Epi e) {
-    __shared__ float red[4];
-    const int64_t nc = blockIdx.x;
-    const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
-    const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
-    const float dv = e.d ? e.d[nc] : 1.f;
-    const float bv = e.bias ? e.bias[o] : 0.f;
-    const float* gp = g + nc * hw;
-    const float* up = u + nc * hw;
-    const float* np_ = e.noise ? e.noise + n * e.noise_nstride : nullptr;
-    float part[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t p0 = threadIdx.x; p0 < hw; p0 += 256 * 4) {
-        float uv[4], gv[4], nv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t p = p0 + 256 * k;
-            const int64_t pp = p < hw ? p : 0;
-            uv[k] = up[pp];
-            gv[k] = gp[pp];
-            nv[k] = np_ ? np_[pp] : 0.f;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (p0 + 256 * k >= hw) continue;
-            const float yv = smc::epi_y(uv[k], dv, nv[k] * nstr, bv, e.act, e.alpha, e.gain, e.clamp);
-            part[k] += smc::act_grad_y(e.act, gv[k], yv, e.alpha, e.gain, e.clamp) * uv[k];
-        }
-    }
-    const float tot = block_sum256((part[0] + part[1]) + (part[2] + part[3]), red);
-    if (threadIdx.x == 0) dd[nc] += tot;
+// dd[n, o] += the plane's per-tile partials (the act / FIR backward kernels' block sums, Epi::dd_part), one wave per
+// plane in a fixed order (lane-strided sums, then a fixed butterfly): the style gradient of the demodulation is
+// bit-reproducible whatever the plane size.  The fused kernels add their partials with float atomics directly only
+// while a plane has at most two dd-owning tiles (two addends onto zero commute) -- every trainable layer of
+// find_direction (b8..b64); larger planes (the latent mapper's high-resolution styles) take this two-level sum.
+__global__ __launch_bounds__(256) void dd_sum_kernel(const float* part, int64_t tiles, float* dd, int64_t planes) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nc = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (nc >= planes) return;
+    const float* p = part + nc * tiles;
+    float acc = 0.f;
+    for (int64_t t = lane; t < tiles; t += 64) acc += p[t];
+    acc = wave_sum(acc);
+    if (lane == 0) dd[nc] += acc;
 }
 
 // float4 form (hw % 4 == 0): each thread owns AB_V float4 groups of one plane, all loads issued first.
@@ -792,9 +780,12 @@ __global__ __launch_bounds__(256) void act_bwd_vec4_kernel(const float* g, const
         }
         du4[q] = make_float4(r[0], r[1], r[2], r[3]);
     }
-    if (dd) {
+    if (dd || e.dd_part) {
         const float tot = block_sum256(part, red);
-        if (threadIdx.x == 0) atomicAdd(dd + nc, tot);
+        if (threadIdx.x == 0) {
+            if (e.dd_part) e.dd_part[nc * gridDim.x + blockIdx.x] = tot;
+            else atomicAdd(dd + nc, tot);
+        }
     }
 }
 
@@ -959,24 +950,40 @@ SMC_API int smc_modconv_act_bwd_f32(const float* g, const float* u, float* du, f
     const bool vec4 = hw % 4 == 0 && (from_y || !epi->noise || epi->noise_nstride % 4 == 0) && align % 16 == 0;
     // more than two workgroups per plane: dd from the one-workgroup-per-plane pass (deterministic order)
     const int64_t blocks_per_plane = vec4 ? smc::ceil_div(hw / 4, 256 * AB_V) : std::max<int64_t>(1, smc::ceil_div(hw, 256 * 8));
-    if (dd && blocks_per_plane > 2) {
-        const int rc = smc_modconv_act_bwd_f32(g, u, du, nullptr, n, c, h, w, epi, stream);
-        if (rc != SMC_OK) return rc;
-        hipLaunchKernelGGL(dd_plane_kernel, dim3((unsigned)planes), dim3(256), 0, st, g, u, dd, c, hw, to_epi(epi));
-        return smc::check_launch("smc_modconv_act_bwd_f32 (dd)");
+    // more than two workgroups per plane: per-workgroup dd partials, summed per plane in a fixed order
+    Epi e = to_epi(epi);
+    float* ddk = dd;
+    const bool two_level = dd && blocks_per_plane > 2;
+    if (two_level) {
+        if (hipMallocAsync(reinterpret_cast<void**>(&e.dd_part), sizeof(float) * planes * blocks_per_plane, st) !=
+            hipSuccess) {
+            smc::set_error("smc_modconv_act_bwd_f32: dd partials allocation failed");
+            return SMC_ERR_LAUNCH;
+        }
+        ddk = nullptr;
     }
     if (vec4) {
-        const dim3 grid((unsigned)smc::ceil_div(hw / 4, 256 * AB_V), (unsigned)planes);
-        if (from_y) hipLaunchKernelGGL(act_bwd_vec4_kernel<true>, grid, dim3(256), 0, st, g, u, du, dd, c, hw, to_epi(epi));
-        else hipLaunchKernelGGL(act_bwd_vec4_kernel<false>, grid, dim3(256), 0, st, g, u, du, dd, c, hw, to_epi(epi));
-        return smc::check_launch("smc_modconv_act_bwd_f32");
+        const dim3 grid((unsigned)blocks_per_plane, (unsigned)planes);
+        if (from_y) hipLaunchKernelGGL(act_bwd_vec4_kernel<true>, grid, dim3(256), 0, st, g, u, du, ddk, c, hw, e);
+        else hipLaunchKernelGGL(act_bwd_vec4_kernel<false>, grid, dim3(256), 0, st, g, u, du, ddk, c, hw, e);
+    } else {
+        const dim3 grid((unsigned)blocks_per_plane, (unsigned)planes);
+        if (from_y) hipLaunchKernelGGL(act_bwd_kernel<true>, grid, dim3(256), 0, st, g, u, du, ddk, c, hw, e);
+        else hipLaunchKernelGGL(act_bwd_kernel<false>, grid, dim3(256), 0, st, g, u, du, ddk, c, hw, e);
     }
-    int64_t per_plane = smc::ceil_div(hw, 256 * 8);  // ~8 elements per thread
-    if (per_plane < 1) per_plane = 1;
-    const dim3 grid((unsigned)per_plane, (unsigned)planes);
-    if (from_y) hipLaunchKernelGGL(act_bwd_kernel<true>, grid, dim3(256), 0, st, g, u, du, dd, c, hw, to_epi(epi));
-    else hipLaunchKernelGGL(act_bwd_kernel<false>, grid, dim3(256), 0, st, g, u, du, dd, c, hw, to_epi(epi));
-    return smc::check_launch("smc_modconv_act_bwd_f32");
+    int rc = smc::check_launch("smc_modconv_act_bwd_f32");
+    if (two_level) {
+        if (rc == SMC_OK) {
+            hipLaunchKernelGGL(dd_sum_kernel, dim3((unsigned)smc::ceil_div(planes, 4)), dim3(256), 0, st, e.dd_part,
+                               blocks_per_plane, dd, planes);
+            rc = smc::check_launch("smc_modconv_act_bwd_f32 (dd)");
+        }
+        if (hipFreeAsync(e.dd_part, st) != hipSuccess && rc == SMC_OK) {
+            smc::set_error("smc_modconv_act_bwd_f32: dd partials release failed");
+            rc = SMC_ERR_LAUNCH;
+        }
+    }
+    return rc;
 }
 
 SMC_API int smc_channel_dot_f32(const float* a, const float* b, const float* scale, float* out, float* a_scaled,
@@ -1022,18 +1029,20 @@ SMC_API int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* 
     const bool from_y = epi->grad_from_y != 0;
     SMC_CHECK(!from_y || !dd, "smc_modconv_blur_act_bwd_f32: dd needs u (grad_from_y set)");
     hipStream_t st = smc::as_stream(stream);
-    // dd-owning tiles per plane (each tile owns its 32 x 64 window of the u plane): more than two -> the fused kernel
-    // runs without dd and the one-workgroup-per-plane pass adds it (deterministic order)
-    if (dd && smc::ceil_div(u_h, kFH) * smc::ceil_div(u_w, kFW) > 2) {
-        const int rc = smc_modconv_blur_act_bwd_f32(g, u, dt, nullptr, n, c, u_h, u_w, t_h, t_w, t_pitch, f, fh, fw,
-                                                    padx0, pady0, fgain, flip, epi, stream);
-        if (rc != SMC_OK) return rc;
-        hipLaunchKernelGGL(dd_plane_kernel, dim3((unsigned)((int64_t)n * c)), dim3(256), 0, st, g, u, dd, c,
-                           (int64_t)u_h * u_w, to_epi(epi));
-        return smc::check_launch("smc_modconv_blur_act_bwd_f32 (dd)");
-    }
     const dim3 grid = fir_grid_bwd((int64_t)n * c, t_w, t_h);
-    const Epi e = to_epi(epi);
+    Epi e = to_epi(epi);
+    // dd-owning tiles per plane (each tile owns its 32 x 64 window of the u plane): more than two -> per-tile partials,
+    // summed per plane in a fixed order after the fused kernel
+    const int64_t planes = (int64_t)n * c, tiles = (int64_t)grid.y * grid.z;
+    float* const dd_out = dd;
+    const bool two_level = dd && smc::ceil_div(u_h, kFH) * smc::ceil_div(u_w, kFW) > 2;
+    if (two_level) {
+        if (hipMallocAsync(reinterpret_cast<void**>(&e.dd_part), sizeof(float) * planes * tiles, st) != hipSuccess) {
+            smc::set_error("smc_modconv_blur_act_bwd_f32: dd partials allocation failed");
+            return SMC_ERR_LAUNCH;
+        }
+        dd = nullptr;
+    }
     const uintptr_t al = (uintptr_t)g | (uintptr_t)u | (uintptr_t)(from_y ? nullptr : epi->noise);
     const int64_t nstr = from_y ? 0 : epi->noise_nstride;
 #define SMC_BLUR_BWD(KERNEL)                                                                                       \
@@ -1050,5 +1059,17 @@ SMC_API int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* 
         else SMC_BLUR_BWD((blur_act_bwd_fast<4, 4, false, false>));
     }
 #undef SMC_BLUR_BWD
-    return smc::check_launch("smc_modconv_blur_act_bwd_f32");
+    int rc = smc::check_launch("smc_modconv_blur_act_bwd_f32");
+    if (two_level) {
+        if (rc == SMC_OK) {
+            hipLaunchKernelGGL(dd_sum_kernel, dim3((unsigned)smc::ceil_div(planes, 4)), dim3(256), 0, st, e.dd_part,
+                               tiles, dd_out, planes);
+            rc = smc::check_launch("smc_modconv_blur_act_bwd_f32 (dd)");
+        }
+        if (hipFreeAsync(e.dd_part, st) != hipSuccess && rc == SMC_OK) {
+            smc::set_error("smc_modconv_blur_act_bwd_f32: dd partials release failed");
+            rc = SMC_ERR_LAUNCH;
+        }
+    }
+    return rc;
 }
