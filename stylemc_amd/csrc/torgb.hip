@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void torgb_act_bwd_kernel(const float* g_rgb, 
                                                             const float* s, float clamp_rgb, const float* g_next,
                                                             const float* y, float* du, int cin, int cout, int64_t hw,
                                                             const float* d, int act, float alpha, float gain,
-                                                            float clamp) {
+                                                            float clamp, int kch) {
     __shared__ float ws[kMaxOut * kMaxIn];
     const int nn = blockIdx.y;
     for (int i = threadIdx.x; i < cout * cin; i += 256) {
@@ -174,14 +174,16 @@ __global__ __launch_bounds__(256) void torgb_act_bwd_kernel(const float* g_rgb, 
         }
     }
     const int64_t base = (int64_t)nn * cin * hw + p0;
+    // this workgroup's channels: grid.z splits them when the position grid alone is small (kch = cin otherwise)
+    const int kbeg = blockIdx.z * kch, kend = min(cin, kbeg + kch);
     // Channels in chunks of KC: every load of a chunk is issued before its stores (one at a time, each channel's
     // loads would wait for the previous channel's store: vmcnt counts both).
     constexpr int KC = 8;
-    for (int k0 = 0; k0 < cin; k0 += KC) {
+    for (int k0 = kbeg; k0 < kend; k0 += KC) {
         float gn[KC][V], yk[KC][V], dkv[KC];
 #pragma unroll
         for (int kk = 0; kk < KC; ++kk) {
-            const int k = min(k0 + kk, cin - 1);
+            const int k = min(k0 + kk, kend - 1);
             const int64_t off = base + (int64_t)k * hw;
             dkv[kk] = d ? d[(int64_t)nn * cin + k] : 1.f;
             if (VEC) {
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(256) void torgb_act_bwd_kernel(const float* g_rgb, 
 #pragma unroll
         for (int kk = 0; kk < KC; ++kk) {
             const int k = k0 + kk;
-            if (k >= cin) break;
+            if (k >= kend) break;
             const int64_t off = base + (int64_t)k * hw;
             const float dk = dkv[kk];
             float r[V];
@@ -380,11 +382,20 @@ SMC_API int smc_torgb_act_bwd_f32(const float* g_rgb, const float* y_rgb, const 
     const bool vec = hw % 4 == 0 && (al & 15) == 0;
     const int64_t per = vec ? hw / 4 : hw;
     dim3 grid((unsigned)smc::ceil_div(per, 256), (unsigned)n);
+    // Each thread walks its positions' channels one 8-channel chunk after another (a chain of dependent load rounds):
+    // a small position grid (the 128..512-px blocks) also splits the channels over grid.z, in whole chunks, until the
+    // launch holds ~4 workgroups per CU (r = 128: 64 workgroups walking 256 channels took 264 us).
+    int nz = 1;
+    while ((int64_t)grid.x * grid.y * nz < 4 * (int64_t)smc::device_cu_count() && cin % (16 * nz) == 0) nz *= 2;
+    grid.z = (unsigned)nz;
+    const int kch = cin / nz;
     if (vec)
         hipLaunchKernelGGL(torgb_act_bwd_kernel<true>, grid, dim3(256), 0, smc::as_stream(stream), g_rgb, y_rgb, w, s,
-                           clamp_rgb, g_next, y, du, cin, cout, hw, epi->d, epi->act, epi->alpha, epi->gain, epi->clamp);
+                           clamp_rgb, g_next, y, du, cin, cout, hw, epi->d, epi->act, epi->alpha, epi->gain, epi->clamp,
+                           kch);
     else
         hipLaunchKernelGGL(torgb_act_bwd_kernel<false>, grid, dim3(256), 0, smc::as_stream(stream), g_rgb, y_rgb, w, s,
-                           clamp_rgb, g_next, y, du, cin, cout, hw, epi->d, epi->act, epi->alpha, epi->gain, epi->clamp);
+                           clamp_rgb, g_next, y, du, cin, cout, hw, epi->d, epi->act, epi->alpha, epi->gain, epi->clamp,
+                           kch);
     return smc::check_launch("smc_torgb_act_bwd_f32");
 }
