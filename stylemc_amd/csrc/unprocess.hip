@@ -105,37 +105,98 @@ __device__ __forceinline__ int taps_of(int i, int in, int out, float scale, int 
     return n;
 }
 
+// taps_of in a fixed-size form: the candidate outputs d0 .. d0 + 4 of input index i, bit t of `mask` set when
+// output d0 + t reads i (w[t] its combined weight) -- the same entries in the same order as taps_of, but with
+// compile-time indices, so the per-column tables stay in registers.
+struct Taps5 {
+    int d0;
+    unsigned mask;
+    float w[5];
+};
+
+__device__ __forceinline__ Taps5 taps5(int i, int in, int out, float scale) {
+    Taps5 t;
+    t.d0 = (int)floorf((i + 0.5f) / scale - 0.5f) - 2;
+    t.mask = 0;
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+        const int d = t.d0 + u;
+        t.w[u] = 0.f;
+        if (d < 0 || d >= out) continue;
+        const float r = scale * (d + 0.5f) - 0.5f;
+        const int f = (int)floorf(r);
+        float c[4];
+        cubic_coeffs(r - f, c);
+        float acc = 0.f;
+        bool hit = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (min(max(f - 1 + k, 0), in - 1) == i) {
+                acc += c[k];
+                hit = true;
+            }
+        }
+        if (hit) {
+            t.w[u] = acc;
+            t.mask |= 1u << u;
+        }
+    }
+    return t;
+}
+
+// One workgroup per band of UB_R rows of one plane, UB_C consecutive 256-column strides per thread: the column taps
+// depend only on the column and are computed once per workgroup (not once per pixel), the row taps once per row and
+// thread.  Per pixel the terms and their order are those of the one-thread-per-pixel form (gather over the outputs
+// whose taps read the pixel, rows outer), so dimg is bit-identical.
+constexpr int UB_R = 8, UB_C = 4;
+
 template <int MODE>
 __global__ __launch_bounds__(256) void unprocess_bwd_kernel(const float* img, const float* dy, float* dimg,
                                                             int64_t planes, Unproc q) {
-    const int64_t per = (int64_t)q.in_h * q.in_w;
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= planes * per) return;
-    const int64_t pl = idx / per;
-    const int rem = (int)(idx - pl * per);
-    const int yy = rem / q.in_w, xx = rem - yy * q.in_w;
-    int oy[8], ox[8];
-    float wy[8], wx[8];
-    const int ny = taps_of(yy, q.in_h, q.out_h, q.sy, oy, wy);
-    float g = 0.f;
-    if (ny > 0) {
-        const int nx = taps_of(xx, q.in_w, q.out_w, q.sx, ox, wx);
-        const float* d = dy + pl * (int64_t)q.out_h * q.out_w;
-        for (int a = 0; a < ny; ++a) {
-            float r = 0.f;
-            for (int b = 0; b < nx; ++b) r += d[(int64_t)oy[a] * q.out_w + ox[b]] * wx[b];
-            g += r * wy[a];
+    const int bands = (q.in_h + UB_R - 1) / UB_R;
+    const int64_t pl = blockIdx.x / bands;
+    const int r0 = (int)(blockIdx.x - pl * bands) * UB_R;
+    const int c = (int)(pl % q.channels);
+    const float* d = dy + pl * (int64_t)q.out_h * q.out_w;
+    const int64_t pbase = pl * (int64_t)q.in_h * q.in_w;
+    for (int k0 = 0; k0 * 256 < q.in_w; k0 += UB_C) {
+        Taps5 tx[UB_C];
+#pragma unroll
+        for (int k = 0; k < UB_C; ++k) {
+            const int xx = threadIdx.x + 256 * (k0 + k);
+            tx[k] = taps5(min(xx, q.in_w - 1), q.in_w, q.out_w, q.sx);
         }
-        const int c = (int)(pl % q.channels);
-        if (MODE == 0) {
-            const float x = __fadd_rn(__fmul_rn(img[idx], 127.5f), 128.f);
-            // d/dimg of (pre(img) / 255 - mean) / std; torch.clamp passes the gradient at the bounds
-            g = (x >= 0.f && x <= 255.f) ? g / q.std_[c] / 255.f * 127.5f : 0.f;
-        } else {
-            g = g / q.std_[c] * 0.5f;  // d/dimg of ((img + 1) / 2 - mean) / std after the (linear) resize
+        for (int yy = r0; yy < min(r0 + UB_R, q.in_h); ++yy) {
+            const Taps5 ty = taps5(yy, q.in_h, q.out_h, q.sy);
+#pragma unroll
+            for (int k = 0; k < UB_C; ++k) {
+                const int xx = threadIdx.x + 256 * (k0 + k);
+                if (xx >= q.in_w) continue;
+                const int64_t idx = pbase + (int64_t)yy * q.in_w + xx;
+                float g = 0.f;
+                if (ty.mask) {
+#pragma unroll
+                    for (int a = 0; a < 5; ++a) {
+                        if (!((ty.mask >> a) & 1u)) continue;
+                        const float* drow = d + (int64_t)(ty.d0 + a) * q.out_w;
+                        float r = 0.f;
+#pragma unroll
+                        for (int bb = 0; bb < 5; ++bb)
+                            if ((tx[k].mask >> bb) & 1u) r += drow[tx[k].d0 + bb] * tx[k].w[bb];
+                        g += r * ty.w[a];
+                    }
+                    if (MODE == 0) {
+                        const float x = __fadd_rn(__fmul_rn(img[idx], 127.5f), 128.f);
+                        // d/dimg of (pre(img) / 255 - mean) / std; torch.clamp passes the gradient at the bounds
+                        g = (x >= 0.f && x <= 255.f) ? g / q.std_[c] / 255.f * 127.5f : 0.f;
+                    } else {
+                        g = g / q.std_[c] * 0.5f;  // d/dimg of ((img + 1) / 2 - mean) / std after the (linear) resize
+                    }
+                }
+                dimg[idx] = g;
+            }
         }
     }
-    dimg[idx] = g;
 }
 
 }  // namespace
@@ -163,8 +224,9 @@ int preprocess_bwd(const char* name, const float* img, const float* dy, int n, i
     const Unproc q{in_h, in_w, out_h, out_w, channels, (float)in_h / (float)out_h, (float)in_w / (float)out_w, mean,
                    std_};
     const int64_t planes = (int64_t)n * channels;
-    hipLaunchKernelGGL(unprocess_bwd_kernel<MODE>, dim3((unsigned)smc::ceil_div(planes * in_h * in_w, 256)),
-                       dim3(256), 0, smc::as_stream(stream), img, dy, dimg, planes, q);
+    const int64_t blocks = planes * smc::ceil_div(in_h, UB_R);
+    hipLaunchKernelGGL(unprocess_bwd_kernel<MODE>, dim3((unsigned)blocks), dim3(256), 0, smc::as_stream(stream), img, dy,
+                       dimg, planes, q);
     return smc::check_launch(name);
 }
 
