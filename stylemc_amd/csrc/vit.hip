@@ -780,12 +780,21 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* x, int64_t ldx
         q += d * d;
     }
     const float rstd = rsqrtf(wave_sum(q) / D + eps);
+    // the affine parameters loaded before the first store (loaded next to each store, every column waited out the
+    // previous column's store: vmcnt counts both)
+    float wv[LN_MAXV], bv[LN_MAXV];
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) {
+        const int c = lane + 64 * min(t, nv - 1);
+        wv[t] = w[c];
+        bv[t] = b[c];
+    }
     float* yr = y + row * ldy;
 #pragma unroll
     for (int t = 0; t < LN_MAXV; ++t) {
         if (t >= nv) break;
         const int c = lane + 64 * t;
-        yr[c] = (v[t] - mean) * rstd * w[c] + b[c];
+        yr[c] = (v[t] - mean) * rstd * wv[t] + bv[t];
     }
     if (lane == 0) {
         if (mean_out) mean_out[row] = mean;
@@ -817,12 +826,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* dy, int64_t ld
         s2 += g[t] * xh[t];
     }
     const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
+    float rv[LN_MAXV];  // the residual gradient loaded before the first store (as in ln_fwd_kernel)
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) rv[t] = dres ? dres[row * ldres + lane + 64 * min(t, nv - 1)] : 0.f;
 #pragma unroll
     for (int t = 0; t < LN_MAXV; ++t) {
         if (t >= nv) break;
         const int c = lane + 64 * t;
         float v = rstd * (g[t] - m1 - xh[t] * m2);
-        if (dres) v += dres[row * ldres + c];
+        if (dres) v += rv[t];
         dx[row * lddx + c] = v;
     }
 }
