@@ -80,6 +80,8 @@ __global__ __launch_bounds__(256) void channel_affine_kernel(const float* x, con
 // out = r * g + shortcut (shortcut = sc (conv path) or x[n, c, s*y, s*x] (MaxPool2d(1, s))) and, optionally,
 // xbn = out * a[c] + b[c] (BN1 of the next unit).  h (channel block 0) and g are stored for the backward.
 constexpr int kSeCpb = 16;
+constexpr int SE_RG = 4;    // excitation rows per wave in flight
+constexpr int SE_MAXQ = 8;  // channels per lane (C <= 512, checked at pack time)
 // pixel-range split of a plane for the SE kernels: at most 256 pixels (one per thread) of each of the kSeCpb channels
 // per workgroup
 inline unsigned se_zsplit(int64_t hw) { return (unsigned)std::max<int64_t>(1, smc::ceil_div(hw, 256)); }
@@ -120,12 +122,27 @@ __global__ __launch_bounds__(256) void se_fwd_combine_kernel(const float* m, con
     }
     for (int c = tid; c < C; c += 256) ms[c] = m[(int64_t)n * C + c];
     __syncthreads();
-    for (int j = wave; j < hid; j += 4) {
-        float t = 0.f;
-#pragma unroll 8
-        for (int c = lane; c < C; c += 64) t += w1[(int64_t)j * C + c] * ms[c];
-        t = wsum(t);
-        if (lane == 0) hs[j] = t > 0.f ? t : 0.f;
+    // excitation layer 1, SE_RG rows per wave at a time with all their weight loads in flight (one row at a time, each
+    // row's loads waited out a round trip: hid / 4 of them per workgroup)
+    for (int j0 = wave; j0 < hid; j0 += 4 * SE_RG) {
+        float wv[SE_RG][SE_MAXQ];
+#pragma unroll
+        for (int r = 0; r < SE_RG; ++r)
+#pragma unroll
+            for (int q = 0; q < SE_MAXQ; ++q) {
+                const int j = min(j0 + 4 * r, hid - 1), c = min(lane + 64 * q, C - 1);
+                wv[r][q] = w1[(int64_t)j * C + c];
+            }
+#pragma unroll
+        for (int r = 0; r < SE_RG; ++r) {
+            float t = 0.f;
+#pragma unroll
+            for (int q = 0; q < SE_MAXQ; ++q)
+                if (lane + 64 * q < C) t += wv[r][q] * ms[lane + 64 * q];
+            t = wsum(t);
+            const int j = j0 + 4 * r;
+            if (lane == 0 && j < hid) hs[j] = t > 0.f ? t : 0.f;
+        }
     }
     __syncthreads();
     if (tid < kSeCpb) {
@@ -177,12 +194,25 @@ __global__ __launch_bounds__(256) void se_bwd_dr_kernel(const float* dg, const f
         dz[c] = dg[(int64_t)n * C + c] * gv * (1.f - gv);
     }
     __syncthreads();
-    for (int j = wave; j < hid; j += 4) {
-        float t = 0.f;
-#pragma unroll 8
-        for (int c = lane; c < C; c += 64) t += w2[(int64_t)c * hid + j] * dz[c];
-        t = wsum(t);
-        if (lane == 0) dh[j] = h[(int64_t)n * hid + j] > 0.f ? t : 0.f;
+    for (int j0 = wave; j0 < hid; j0 += 4 * SE_RG) {  // SE_RG rows at a time, loads first (se_fwd_combine_kernel)
+        float wv[SE_RG][SE_MAXQ], hv[SE_RG];
+#pragma unroll
+        for (int r = 0; r < SE_RG; ++r) {
+            const int j = min(j0 + 4 * r, hid - 1);
+            hv[r] = h[(int64_t)n * hid + j];
+#pragma unroll
+            for (int q = 0; q < SE_MAXQ; ++q) wv[r][q] = w2[(int64_t)min(lane + 64 * q, C - 1) * hid + j];
+        }
+#pragma unroll
+        for (int r = 0; r < SE_RG; ++r) {
+            float t = 0.f;
+#pragma unroll
+            for (int q = 0; q < SE_MAXQ; ++q)
+                if (lane + 64 * q < C) t += wv[r][q] * dz[lane + 64 * q];
+            t = wsum(t);
+            const int j = j0 + 4 * r;
+            if (lane == 0 && j < hid) dh[j] = hv[r] > 0.f ? t : 0.f;
+        }
     }
     __syncthreads();
     if (tid < kSeCpb) {
@@ -337,6 +367,7 @@ int net_validate(const smc_irse_net* net, int n) {
         SMC_CHECK(u.in_h % u.stride == 0 && u.in_w % u.stride == 0, "smc_irse: unit %d odd size", k);
         SMC_CHECK(u.se_hidden >= 1 && u.se_w1 && u.se_w2 && u.bn1_a && u.bn2_a && u.prelu, "smc_irse: unit %d", k);
         SMC_CHECK(u.depth % kSeCpb == 0, "smc_irse: unit %d depth %d not a multiple of %d", k, u.depth, kSeCpb);
+        SMC_CHECK(u.depth <= 64 * SE_MAXQ, "smc_irse: unit %d depth %d > %d", k, u.depth, 64 * SE_MAXQ);
         SMC_CHECK(u.se_hidden <= 256, "smc_irse: unit %d SE hidden width %d > 256", k, u.se_hidden);
         SMC_CHECK(u.sc_conv || u.cin == u.depth, "smc_irse: unit %d identity shortcut needs cin == depth", k);
         SMC_CHECK(u.c2_bwd_nphases == (u.stride == 2 ? 4 : 1), "smc_irse: unit %d adjoint phases", k);
