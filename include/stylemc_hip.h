@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 3
+#define SMC_ABI_VERSION 4
 
 #define SMC_OK 0
 #define SMC_ERR_INVALID 1     /* bad argument / shape (reference: TORCH_CHECK -> RuntimeError)   */
@@ -206,7 +206,11 @@ int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_stride, f
  * (SMC_ERR_UNSUPPORTED otherwise). */
 int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* dt, float* dd, int n, int c, int u_h, int u_w,
                                  int t_h, int t_w, int t_pitch, const float* f, int fh, int fw, int padx0, int pady0,
-                                 float fgain, int flip, const smc_conv_epilogue* epi, void* stream);
+                                 float fgain, int flip, const smc_conv_epilogue* epi, void* workspace,
+                                 int64_t workspace_bytes, void* stream);
+/* Workspace smc_modconv_blur_act_bwd_f32 needs when dd != NULL (0: none; the per-tile dd partials of planes wider
+ * than two FIR tiles, summed per plane in a fixed order -- bit-reproducible dd). */
+int64_t smc_modconv_blur_act_bwd_workspace_size(int n, int c, int u_h, int u_w, int t_h, int t_w);
 
 /* d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps), wsq[o,i] = sum_k W[o,i,k]^2 (demodulation). */
 int smc_modconv_demod_f32(const float* s, const float* wsq, float* d, int n, int cin, int cout, float eps,
@@ -215,7 +219,10 @@ int smc_modconv_demod_f32(const float* s, const float* wsq, float* d, int n, int
 /* Backward of the modconv epilogue: recompute y from u, dz = bias_act grad (CUDA-kernel semantics,
  * bias_act.cu:51-142), du = dz * d[n,o]; if dd != NULL: dd[n,o] += sum_hw dz*u. */
 int smc_modconv_act_bwd_f32(const float* g, const float* u, float* du, float* dd, int n, int c, int h, int w,
-                            const smc_conv_epilogue* epi, void* stream);
+                            const smc_conv_epilogue* epi, void* workspace, int64_t workspace_bytes, void* stream);
+/* Workspace smc_modconv_act_bwd_f32 needs when dd != NULL (0: none; per-workgroup dd partials of planes that span
+ * more than two workgroups). */
+int64_t smc_modconv_act_bwd_workspace_size(int n, int c, int h, int w);
 
 /* out[r] (+)= sum_p a[r,p]*b[r,p] over rows r < rows of length len; if a_scaled != NULL also
  * a_scaled[r,p] = a[r,p]*scale[r] (scale may be NULL only when a_scaled is NULL). */

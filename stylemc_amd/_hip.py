@@ -74,9 +74,11 @@ _SIGS = {
     "smc_modconv_blur_act_f32": (c_int, [P, c_int, c_int64, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                          c_int, c_int, c_int, c_int, c_float, c_int, P, P]),
     "smc_modconv_blur_act_bwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int,
-                                             c_int, c_int, c_int, c_float, c_int, P, P]),
+                                             c_int, c_int, c_int, c_float, c_int, P, P, c_int64, P]),
+    "smc_modconv_blur_act_bwd_workspace_size": (c_int64, [c_int] * 6),
     "smc_modconv_demod_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
-    "smc_modconv_act_bwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P]),
+    "smc_modconv_act_bwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int64, P]),
+    "smc_modconv_act_bwd_workspace_size": (c_int64, [c_int] * 4),
     "smc_channel_dot_f32": (c_int, [P, P, P, P, P, c_int64, c_int64, c_int, P]),
     "smc_modconv_demod_bwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, P]),
     "smc_torgb_fwd_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, P]),
@@ -133,7 +135,7 @@ def load(path=None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.smc_abi_version() != 3:
+        if lib.smc_abi_version() != 4:
             raise RuntimeError("stylemc_amd: ABI version mismatch, rebuild the library")
         if path is None:
             _lib = lib

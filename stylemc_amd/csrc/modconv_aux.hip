@@ -936,8 +936,22 @@ SMC_API int smc_modconv_demod_f32(const float* s, const float* wsq, float* d, in
     return smc::check_launch("smc_modconv_demod_f32");
 }
 
+// dd partials of smc_modconv_act_bwd_f32: one float per (plane, workgroup) when a plane spans more than two
+// workgroups (either load form), summed per plane in a fixed order by dd_sum_kernel.
+static int64_t act_bwd_blocks_per_plane(int64_t hw, bool vec4) {
+    return vec4 ? smc::ceil_div(hw / 4, 256 * AB_V) : std::max<int64_t>(1, smc::ceil_div(hw, 256 * 8));
+}
+
+SMC_API int64_t smc_modconv_act_bwd_workspace_size(int n, int c, int h, int w) {
+    if (n < 1 || c < 1 || h < 1 || w < 1) return 0;
+    const int64_t hw = (int64_t)h * w;
+    const int64_t bpp = std::max(act_bwd_blocks_per_plane(hw, hw % 4 == 0), act_bwd_blocks_per_plane(hw, false));
+    return bpp > 2 ? (int64_t)sizeof(float) * n * c * bpp : 0;
+}
+
 SMC_API int smc_modconv_act_bwd_f32(const float* g, const float* u, float* du, float* dd, int n, int c, int h, int w,
-                                    const smc_conv_epilogue* epi, void* stream) {
+                                    const smc_conv_epilogue* epi, void* workspace, int64_t workspace_bytes,
+                                    void* stream) {
     SMC_CHECK(g && u && du && n >= 1 && c >= 1 && h >= 1 && w >= 1, "smc_modconv_act_bwd_f32: bad args");
     SMC_CHECK(epi && epi->mode == SMC_EPI_MODACT, "smc_modconv_act_bwd_f32: needs a MODACT epilogue");
     const bool from_y = epi->grad_from_y != 0;
@@ -948,18 +962,16 @@ SMC_API int smc_modconv_act_bwd_f32(const float* g, const float* u, float* du, f
     const uintptr_t align = (uintptr_t)g | (uintptr_t)u | (uintptr_t)du | (uintptr_t)(from_y ? nullptr : epi->noise);
     hipStream_t st = smc::as_stream(stream);
     const bool vec4 = hw % 4 == 0 && (from_y || !epi->noise || epi->noise_nstride % 4 == 0) && align % 16 == 0;
-    // more than two workgroups per plane: dd from the one-workgroup-per-plane pass (deterministic order)
-    const int64_t blocks_per_plane = vec4 ? smc::ceil_div(hw / 4, 256 * AB_V) : std::max<int64_t>(1, smc::ceil_div(hw, 256 * 8));
-    // more than two workgroups per plane: per-workgroup dd partials, summed per plane in a fixed order
+    const int64_t blocks_per_plane = act_bwd_blocks_per_plane(hw, vec4);
+    // more than two workgroups per plane: per-workgroup dd partials in the caller's workspace, summed per plane in a
+    // fixed order (two addends onto zero commute, so up to two workgroups add into dd directly)
     Epi e = to_epi(epi);
     float* ddk = dd;
     const bool two_level = dd && blocks_per_plane > 2;
     if (two_level) {
-        if (hipMallocAsync(reinterpret_cast<void**>(&e.dd_part), sizeof(float) * planes * blocks_per_plane, st) !=
-            hipSuccess) {
-            smc::set_error("smc_modconv_act_bwd_f32: dd partials allocation failed");
-            return SMC_ERR_LAUNCH;
-        }
+        SMC_CHECK(workspace && workspace_bytes >= (int64_t)sizeof(float) * planes * blocks_per_plane,
+                  "smc_modconv_act_bwd_f32: dd needs smc_modconv_act_bwd_workspace_size() bytes of workspace");
+        e.dd_part = static_cast<float*>(workspace);
         ddk = nullptr;
     }
     if (vec4) {
@@ -972,16 +984,10 @@ SMC_API int smc_modconv_act_bwd_f32(const float* g, const float* u, float* du, f
         else hipLaunchKernelGGL(act_bwd_kernel<false>, grid, dim3(256), 0, st, g, u, du, ddk, c, hw, e);
     }
     int rc = smc::check_launch("smc_modconv_act_bwd_f32");
-    if (two_level) {
-        if (rc == SMC_OK) {
-            hipLaunchKernelGGL(dd_sum_kernel, dim3((unsigned)smc::ceil_div(planes, 4)), dim3(256), 0, st, e.dd_part,
-                               blocks_per_plane, dd, planes);
-            rc = smc::check_launch("smc_modconv_act_bwd_f32 (dd)");
-        }
-        if (hipFreeAsync(e.dd_part, st) != hipSuccess && rc == SMC_OK) {
-            smc::set_error("smc_modconv_act_bwd_f32: dd partials release failed");
-            rc = SMC_ERR_LAUNCH;
-        }
+    if (two_level && rc == SMC_OK) {
+        hipLaunchKernelGGL(dd_sum_kernel, dim3((unsigned)smc::ceil_div(planes, 4)), dim3(256), 0, st, e.dd_part,
+                           blocks_per_plane, dd, planes);
+        rc = smc::check_launch("smc_modconv_act_bwd_f32 (dd)");
     }
     return rc;
 }
@@ -1011,10 +1017,23 @@ SMC_API int smc_modconv_demod_bwd_f32(const float* s, const float* d, const floa
     return smc::check_launch("smc_modconv_demod_bwd_f32");
 }
 
+// dd partials of smc_modconv_blur_act_bwd_f32: one float per (plane, FIR tile) when more than two tiles of a plane own
+// a part of its u window.
+static int64_t blur_bwd_dd_tiles(int u_h, int u_w, int t_h, int t_w) {
+    if (smc::ceil_div(u_h, kFH) * smc::ceil_div(u_w, kFW) <= 2) return 0;
+    const dim3 grid = fir_grid_bwd(1, t_w, t_h);
+    return (int64_t)grid.y * grid.z;
+}
+
+SMC_API int64_t smc_modconv_blur_act_bwd_workspace_size(int n, int c, int u_h, int u_w, int t_h, int t_w) {
+    if (n < 1 || c < 1 || u_h < 1 || u_w < 1 || t_h < 1 || t_w < 1) return 0;
+    return (int64_t)sizeof(float) * n * c * blur_bwd_dd_tiles(u_h, u_w, t_h, t_w);
+}
+
 SMC_API int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* dt, float* dd, int n, int c, int u_h,
                                          int u_w, int t_h, int t_w, int t_pitch, const float* f, int fh, int fw,
                                          int padx0, int pady0, float fgain, int flip, const smc_conv_epilogue* epi,
-                                         void* stream) {
+                                         void* workspace, int64_t workspace_bytes, void* stream) {
     SMC_CHECK(g && u && dt && f && n >= 1 && c >= 1 && u_h >= 1 && u_w >= 1, "smc_modconv_blur_act_bwd_f32: bad args");
     SMC_CHECK(epi && epi->mode == SMC_EPI_MODACT, "smc_modconv_blur_act_bwd_f32: needs a MODACT epilogue");
     SMC_CHECK(t_h == u_h + 2 * pady0 - fh + 1 && t_w == u_w + 2 * padx0 - fw + 1,
@@ -1031,16 +1050,15 @@ SMC_API int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* 
     hipStream_t st = smc::as_stream(stream);
     const dim3 grid = fir_grid_bwd((int64_t)n * c, t_w, t_h);
     Epi e = to_epi(epi);
-    // dd-owning tiles per plane (each tile owns its 32 x 64 window of the u plane): more than two -> per-tile partials,
-    // summed per plane in a fixed order after the fused kernel
-    const int64_t planes = (int64_t)n * c, tiles = (int64_t)grid.y * grid.z;
+    // dd-owning tiles per plane (each tile owns its 32 x 64 window of the u plane): more than two -> per-tile partials
+    // in the caller's workspace, summed per plane in a fixed order after the fused kernel
+    const int64_t planes = (int64_t)n * c, tiles = blur_bwd_dd_tiles(u_h, u_w, t_h, t_w);
     float* const dd_out = dd;
-    const bool two_level = dd && smc::ceil_div(u_h, kFH) * smc::ceil_div(u_w, kFW) > 2;
+    const bool two_level = dd && tiles > 0;
     if (two_level) {
-        if (hipMallocAsync(reinterpret_cast<void**>(&e.dd_part), sizeof(float) * planes * tiles, st) != hipSuccess) {
-            smc::set_error("smc_modconv_blur_act_bwd_f32: dd partials allocation failed");
-            return SMC_ERR_LAUNCH;
-        }
+        SMC_CHECK(workspace && workspace_bytes >= (int64_t)sizeof(float) * planes * tiles,
+                  "smc_modconv_blur_act_bwd_f32: dd needs smc_modconv_blur_act_bwd_workspace_size() bytes of workspace");
+        e.dd_part = static_cast<float*>(workspace);
         dd = nullptr;
     }
     const uintptr_t al = (uintptr_t)g | (uintptr_t)u | (uintptr_t)(from_y ? nullptr : epi->noise);
@@ -1060,16 +1078,10 @@ SMC_API int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* 
     }
 #undef SMC_BLUR_BWD
     int rc = smc::check_launch("smc_modconv_blur_act_bwd_f32");
-    if (two_level) {
-        if (rc == SMC_OK) {
-            hipLaunchKernelGGL(dd_sum_kernel, dim3((unsigned)smc::ceil_div(planes, 4)), dim3(256), 0, st, e.dd_part,
-                               tiles, dd_out, planes);
-            rc = smc::check_launch("smc_modconv_blur_act_bwd_f32 (dd)");
-        }
-        if (hipFreeAsync(e.dd_part, st) != hipSuccess && rc == SMC_OK) {
-            smc::set_error("smc_modconv_blur_act_bwd_f32: dd partials release failed");
-            rc = SMC_ERR_LAUNCH;
-        }
+    if (two_level && rc == SMC_OK) {
+        hipLaunchKernelGGL(dd_sum_kernel, dim3((unsigned)smc::ceil_div(planes, 4)), dim3(256), 0, st, e.dd_part,
+                           tiles, dd_out, planes);
+        rc = smc::check_launch("smc_modconv_blur_act_bwd_f32 (dd)");
     }
     return rc;
 }

@@ -332,6 +332,17 @@ def _modconv_epi_bwd(ctx, d):
     return epi
 
 
+def _dd_workspace(dd, nbytes, device):
+    """The dd-partials workspace of the epilogue backward kernels (torch's caching allocator, not the library)."""
+    if dd is None or nbytes <= 0:
+        return None
+    return torch.empty(nbytes // 4, device=device, dtype=torch.float32)
+
+
+def _nbytes(t):
+    return 0 if t is None else 4 * t.numel()
+
+
 def _modconv_bwd(ctx, saved, gy, need_dx, need_ds, g=None):
     """The modconv backward from the output gradient gy -- or from g, the epilogue's backward already applied
     (du = act'(gy; y) * d, a 1:1 layer whose styles need no gradient).  Returns (dx, ds)."""
@@ -346,8 +357,10 @@ def _modconv_bwd(ctx, saved, gy, need_dx, need_ds, g=None):
         epi = _modconv_epi_bwd(ctx, d)
         if spec.up == 1:
             g = torch.empty_like(u)
+            ws = _dd_workspace(dd, _hip.load().smc_modconv_act_bwd_workspace_size(n, P.cout, u.shape[2], u.shape[3]),
+                               x.device)
             _hip.call("smc_modconv_act_bwd_f32", gy.data_ptr(), u.data_ptr(), g.data_ptr(), _hip.ptr(dd), n, P.cout,
-                      u.shape[2], u.shape[3], ctypes.byref(epi), _hip.stream())
+                      u.shape[2], u.shape[3], ctypes.byref(epi), _hip.ptr(ws), _nbytes(ws), _hip.stream())
         else:
             # fused: epilogue backward + adjoint of FIR(pad 1, gain 4) (pad fw-1-1 = 2, correlation) + dd
             f = spec.filter.to(x.device)
@@ -357,9 +370,11 @@ def _modconv_bwd(ctx, saved, gy, need_dx, need_ds, g=None):
             th, tw = 2 * h + 1, 2 * w + 1
             pitch = (tw + 3) // 4 * 4
             g = torch.empty(n, P.cout, th, pitch, device=x.device, dtype=torch.float32)
+            ws = _dd_workspace(dd, _hip.load().smc_modconv_blur_act_bwd_workspace_size(n, P.cout, u.shape[2],
+                                                                                        u.shape[3], th, tw), x.device)
             _hip.call("smc_modconv_blur_act_bwd_f32", gy.data_ptr(), u.data_ptr(), g.data_ptr(), _hip.ptr(dd), n,
                       P.cout, u.shape[2], u.shape[3], th, tw, pitch, _hip.ptr(f), fh, fw, fw - 2, fh - 2, 4.0, 1,
-                      ctypes.byref(epi), _hip.stream())
+                      ctypes.byref(epi), _hip.ptr(ws), _nbytes(ws), _hip.stream())
     else:
         assert spec.up == 1 and dd is None
     dx = torch.empty_like(x) if need_dx else None

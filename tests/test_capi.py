@@ -37,7 +37,7 @@ def test_exports_are_only_the_abi():
 
 def test_abi_version_and_errors_without_gpu():
     lib = _hip.load()
-    assert lib.smc_abi_version() == 3
+    assert lib.smc_abi_version() == 4
     # argument validation runs on the host: no GPU needed, must fail loudly with a message
     rc = lib.smc_upfirdn2d_f32(None, None, None, 1, 4, 4, 99, 99, 4, 4, 1, 1, 1, 1, 1, 1, 1, 1, 0, 1.0, None)
     assert rc == 1
@@ -71,3 +71,28 @@ def test_wino_shape_support_without_gpu():
     assert lib.smc_conv3x3_wino_supported(1, 12, 32, 64, 64) == 0       # cin % 8
     assert lib.smc_conv3x3_wino_supported(1, 32, 48, 64, 64) == 0       # cout % 32
     assert lib.smc_conv3x3_wino_supported(16, 512, 512, 256, 256) == 0  # input >= 2 GiB (32-bit buffer offsets)
+
+
+def test_dd_workspace_queries_without_gpu():
+    """The epilogue backward kernels take their dd partials from a caller-owned workspace (no allocation inside the
+    library): the queries are host logic, and a call that needs partials but gets no workspace fails
+    on the host before any launch."""
+    import ctypes
+    lib = _hip.load()
+    # act backward: float4 path 1024 floats per workgroup, scalar 2048 -> partials only beyond two workgroups
+    assert lib.smc_modconv_act_bwd_workspace_size(4, 512, 32, 32) == 0        # 1024 px: one workgroup per plane
+    assert lib.smc_modconv_act_bwd_workspace_size(4, 64, 64, 64) == 0         # 4096 px: 1 (vec4) / 2 workgroups
+    assert lib.smc_modconv_act_bwd_workspace_size(2, 8, 128, 128) == 4 * 16 * 8    # 16384 px: 4 (vec4) / 8 workgroups
+    assert lib.smc_modconv_act_bwd_workspace_size(1, 1, 7, 9) == 0
+    # FIR backward: 32 x 64 u tiles; t tiles over the (2h+1)-wide gradient
+    assert lib.smc_modconv_blur_act_bwd_workspace_size(4, 512, 8, 8, 9, 9) == 0
+    assert lib.smc_modconv_blur_act_bwd_workspace_size(2, 8, 128, 128, 129, 129) == 4 * 16 * (3 * 5)
+    assert lib.smc_modconv_blur_act_bwd_workspace_size(0, 8, 128, 128, 129, 129) == 0
+    epi = _hip.ConvEpilogue()
+    epi.mode = _hip.EPI_MODACT
+    fake = ctypes.c_void_p(256)
+    rc = lib.smc_modconv_act_bwd_f32(fake, fake, fake, fake, 2, 8, 128, 128, ctypes.byref(epi), None, 0, None)
+    assert rc == 1 and b"workspace" in lib.smc_last_error()
+    rc = lib.smc_modconv_blur_act_bwd_f32(fake, fake, fake, fake, 2, 8, 128, 128, 129, 129, 0, fake, 4, 4, 2, 2, 4.0, 1,
+                                          ctypes.byref(epi), fake, 16, None)
+    assert rc == 1 and b"workspace" in lib.smc_last_error()

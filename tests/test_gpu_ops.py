@@ -372,8 +372,9 @@ def test_blur_act_load_paths(n, c, h):
         dt = torch.full((n, c, th, th), float("nan"), device=DEV)
         dd = torch.zeros(n, c, device=DEV)
         epi = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 1.0)
+        ws = _dd_ws("smc_modconv_blur_act_bwd_workspace_size", n, c, r, r, th, th)
         _hip.call("smc_modconv_blur_act_bwd_f32", gb.data_ptr(), ub.data_ptr(), dt.data_ptr(), dd.data_ptr(), n, c,
-                  r, r, th, th, 0, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epi), st)
+                  r, r, th, th, 0, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epi), _hip.ptr(ws), _nb(ws), st)
         return dt, dd
 
     dt0, dd0 = bwd(g, u0)
@@ -385,7 +386,7 @@ def test_blur_act_load_paths(n, c, h):
         epi = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 1.0)
         epi.grad_from_y = 1
         _hip.call("smc_modconv_blur_act_bwd_f32", gb.data_ptr(), yb.data_ptr(), dt.data_ptr(), None, n, c,
-                  r, r, th, th, 0, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epi), st)
+                  r, r, th, th, 0, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epi), None, 0, st)
         return dt
 
     dt2 = bwd_from_y(g, y0)
@@ -401,6 +402,17 @@ def test_blur_act_load_paths(n, c, h):
     # y = epi_y(u) bit for bit, so the mask and dT are identical
     assert torch.equal(dt2, dt0), "dT from y vs from u"
     assert torch.equal(dt3, dt0), "dT from y, scalar loads"
+
+
+def _dd_ws(query, *dims):
+    """The caller-owned dd-partials workspace the epilogue backward kernels ask for (None when they need none)."""
+    from stylemc_amd import _hip
+    nbytes = getattr(_hip.load(), query)(*dims)
+    return torch.empty(nbytes // 4, device=DEV) if nbytes > 0 else None
+
+
+def _nb(t):
+    return 0 if t is None else 4 * t.numel()
 
 
 def _dd_ref(g, u, d, noise, strength, bias, alpha=0.2, gain=2 ** 0.5, clamp=1.0):
@@ -432,12 +444,13 @@ def test_act_bwd_dd_deterministic(hw):
     outs = []
     for _ in range(3):
         du, dd = torch.empty_like(u), torch.zeros(n, c, device=DEV)
+        ws = _dd_ws("smc_modconv_act_bwd_workspace_size", n, c, h, w)
         _hip.call("smc_modconv_act_bwd_f32", g.data_ptr(), u.data_ptr(), du.data_ptr(), dd.data_ptr(), n, c, h, w,
-                  ctypes.byref(epi), _hip.stream())
+                  ctypes.byref(epi), _hip.ptr(ws), _nb(ws), _hip.stream())
         outs.append((du, dd))
     du_n, dd_none = torch.empty_like(u), None
     _hip.call("smc_modconv_act_bwd_f32", g.data_ptr(), u.data_ptr(), du_n.data_ptr(), None, n, c, h, w,
-              ctypes.byref(epi), _hip.stream())
+              ctypes.byref(epi), None, 0, _hip.stream())
     torch.cuda.synchronize()
     for du, dd in outs[1:]:
         assert torch.equal(dd, outs[0][1]) and torch.equal(du, outs[0][0])
@@ -470,8 +483,10 @@ def test_blur_act_bwd_dd_two_level(uhw):
     def run(with_dd):
         dt = torch.zeros(n, c, th, pitch, device=DEV)
         dd = torch.zeros(n, c, device=DEV) if with_dd else None
+        ws = _dd_ws("smc_modconv_blur_act_bwd_workspace_size", n, c, uh, uw, th, tw) if with_dd else None
         _hip.call("smc_modconv_blur_act_bwd_f32", g.data_ptr(), u.data_ptr(), dt.data_ptr(), _hip.ptr(dd), n, c, uh,
-                  uw, th, tw, pitch, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epi), _hip.stream())
+                  uw, th, tw, pitch, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epi), _hip.ptr(ws), _nb(ws),
+                  _hip.stream())
         return dt, dd
 
     outs = [run(True) for _ in range(3)]
@@ -504,16 +519,17 @@ def test_act_bwd_from_y(hw):
     _hip.call("smc_modconv_epilogue_f32", u.data_ptr(), 1, 0, y.data_ptr(), n, c, h, w, ctypes.byref(epi), st)
     du0, du1 = torch.empty_like(u), torch.empty_like(u)
     dd = torch.zeros(n, c, device=DEV)
+    ws = _dd_ws("smc_modconv_act_bwd_workspace_size", n, c, h, w)
     _hip.call("smc_modconv_act_bwd_f32", g.data_ptr(), u.data_ptr(), du0.data_ptr(), dd.data_ptr(), n, c, h, w,
-              ctypes.byref(epi), st)
+              ctypes.byref(epi), _hip.ptr(ws), _nb(ws), st)
     epi.grad_from_y = 1
     _hip.call("smc_modconv_act_bwd_f32", g.data_ptr(), y.data_ptr(), du1.data_ptr(), None, n, c, h, w,
-              ctypes.byref(epi), st)
+              ctypes.byref(epi), None, 0, st)
     torch.cuda.synchronize()
     assert torch.equal(du0, du1)
     with pytest.raises(RuntimeError):   # dd needs u
         _hip.call("smc_modconv_act_bwd_f32", g.data_ptr(), y.data_ptr(), du1.data_ptr(), dd.data_ptr(), n, c, h, w,
-                  ctypes.byref(epi), st)
+                  ctypes.byref(epi), _hip.ptr(ws), _nb(ws), st)
 
 
 def test_conv_gemm_2gib_input_fallback():

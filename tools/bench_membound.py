@@ -62,10 +62,14 @@ def main():
         dt = torch.empty_like(t)
         dd = torch.zeros(n, c, device=dev)
         epib = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 256.0)
+        lib = _hip.load()
+        wsb = max(lib.smc_modconv_blur_act_bwd_workspace_size(n, c, r, r, th, th),
+                  lib.smc_modconv_act_bwd_workspace_size(n, c, r, r))
+        ws = torch.empty(max(wsb // 4, 1), device=dev)
 
         def blur_b():
             _hip.call("smc_modconv_blur_act_bwd_f32", g.data_ptr(), u.data_ptr(), dt.data_ptr(), dd.data_ptr(), n, c,
-                      r, r, th, th, 0, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epib), st)
+                      r, r, th, th, 0, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epib), ws.data_ptr(), wsb, st)
         us = timeit(blur_b)
         byt = 4 * (2 * y.numel() + t.numel())
         print(f"r={r:5d} c={c:4d} blur_act_bwd  {us:8.1f} us  {byt / us / 1e3:7.0f} GB/s")
@@ -74,7 +78,7 @@ def main():
 
         def blur_bp():
             _hip.call("smc_modconv_blur_act_bwd_f32", g.data_ptr(), u.data_ptr(), dtp.data_ptr(), dd.data_ptr(), n, c,
-                      r, r, th, th, tp, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epib), st)
+                      r, r, th, th, tp, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epib), ws.data_ptr(), wsb, st)
         us = timeit(blur_bp)
         print(f"r={r:5d} c={c:4d} blur_act_bwd_pitch{tp} {us:8.1f} us  {byt / us / 1e3:7.0f} GB/s")
         epiy = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 256.0)
@@ -82,14 +86,14 @@ def main():
 
         def blur_by():
             _hip.call("smc_modconv_blur_act_bwd_f32", g.data_ptr(), y.data_ptr(), dtp.data_ptr(), None, n, c,
-                      r, r, th, th, tp, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epiy), st)
+                      r, r, th, th, tp, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epiy), None, 0, st)
         us = timeit(blur_by)
         print(f"r={r:5d} c={c:4d} blur_act_bwd_from_y {us:8.1f} us  {byt / us / 1e3:7.0f} GB/s")
         du = torch.empty_like(y)
 
         def actb():
             _hip.call("smc_modconv_act_bwd_f32", g.data_ptr(), u.data_ptr(), du.data_ptr(), dd.data_ptr(), n, c, r, r,
-                      ctypes.byref(epib), st)
+                      ctypes.byref(epib), ws.data_ptr(), wsb, st)
         us = timeit(actb)
         byt = 4 * 3 * y.numel()
         print(f"r={r:5d} c={c:4d} act_bwd       {us:8.1f} us  {byt / us / 1e3:7.0f} GB/s")
