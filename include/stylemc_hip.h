@@ -41,6 +41,14 @@ extern "C" {
 #define SMC_ACT_SWISH 9
 
 int smc_abi_version(void);
+
+/* Batch-invariant planning.  Split-K factors, tile configurations and channel splits are normally chosen per call
+ * to fill the chip, so the same image computed in a batch of 2 and in a batch of 4 may be summed in a different fp32
+ * order.  After smc_set_plan_batch(plan, local) every such decision for a call on n images (m rows of a token-major
+ * GEMM) is made as for n * plan / local images (m * plan / local rows): a data-parallel shard of `local` images of
+ * a `plan`-image batch then computes each image bit for bit as the whole batch does.  (0, 0) restores the default.
+ * Process-wide; set it from the thread that enqueues the work, before enqueueing it. */
+int smc_set_plan_batch(int plan, int local);
 const char* smc_last_error(void);
 
 /* ---------------------------------------------------------------------------------------------
@@ -134,6 +142,9 @@ typedef struct {
 } smc_conv_epilogue;
 
 /* bytes of workspace smc_conv_gemm_f32 needs for these sizes (0 = none). */
+/* 1 if the last smc_conv_gemm_f32 call of this thread launched the split-bf16 kernels (the phases carried wk_x3 and
+ * the LDS-DMA tiles took the shape), 0 if it ran exact-fp32 products (timing / roofline attribution). */
+int smc_conv_gemm_last_x3(void);
 int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, int y_w, const smc_conv_phase* phases,
                                      int nphases);
 
@@ -211,6 +222,18 @@ int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* dt, floa
 /* Workspace smc_modconv_blur_act_bwd_f32 needs when dd != NULL (0: none; the per-tile dd partials of planes wider
  * than two FIR tiles, summed per plane in a fixed order -- bit-reproducible dd). */
 int64_t smc_modconv_blur_act_bwd_workspace_size(int n, int c, int u_h, int u_w, int t_h, int t_w);
+
+/* Loss-head row reductions, one wave per row in a fixed order: the same row gives the same bits in any batch
+ * (PyTorch's row reductions pick their block shape from the row count).  out[r] = sum_k a[r,k] * b[r,k]; ldb = 0
+ * broadcasts b's first row.  Replaces the sums / norms of clip_loss.py:28-34, id_loss.py:26-39, model_irse.py:48. */
+int smc_row_dot_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* out, int rows, int len,
+                    void* stream);
+
+/* The directional CLIP head (clip_loss.py:28-34) per row: f = e - src, u = f / |f|,
+ * loss[r] = 1 - cosine_similarity(u, t) (eps as torch's), grad[r] = d loss[r] / d e[r] = (cos uh - th) / |f|
+ * ([rows, len], dense).  t: one row (the normalised text direction).  len <= 1024. */
+int smc_direction_head_f32(const float* e, int64_t lde, const float* src, int64_t lds, const float* t, float* loss,
+                           float* grad, int rows, int len, float eps, void* stream);
 
 /* d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps), wsq[o,i] = sum_k W[o,i,k]^2 (demodulation). */
 int smc_modconv_demod_f32(const float* s, const float* wsq, float* d, int n, int cin, int cout, float eps,

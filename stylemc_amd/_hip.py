@@ -4,6 +4,7 @@ The library is loaded after ``import torch`` so its ``libamdhip64.so.7`` depende
 HIP runtime torch already loaded (one runtime, so torch's streams are valid handles here).
 There is no fallback: if the library is missing or a call fails, a RuntimeError is raised.
 """
+import contextlib
 import ctypes
 import os
 import threading
@@ -49,6 +50,8 @@ LIN_ACT_NONE, LIN_ACT_QUICKGELU = 0, 1
 P = c_void_p
 _SIGS = {
     "smc_abi_version": (c_int, []),
+    "smc_set_plan_batch": (c_int, [c_int, c_int]),
+    "smc_conv_gemm_last_x3": (c_int, []),
     "smc_last_error": (c_char_p, []),
     "smc_bias_act_f32": (c_int, [P, P, P, P, P, P, c_int64, c_int64, c_int64, c_int, c_int, c_float, c_float, c_float,
                                  P]),
@@ -77,6 +80,8 @@ _SIGS = {
                                              c_int, c_int, c_int, c_float, c_int, P, P, c_int64, P]),
     "smc_modconv_blur_act_bwd_workspace_size": (c_int64, [c_int] * 6),
     "smc_modconv_demod_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
+    "smc_row_dot_f32": (c_int, [P, c_int64, P, c_int64, P, c_int, c_int, P]),
+    "smc_direction_head_f32": (c_int, [P, c_int64, P, c_int64, P, P, P, c_int, c_int, c_float, P]),
     "smc_modconv_act_bwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int64, P]),
     "smc_modconv_act_bwd_workspace_size": (c_int64, [c_int] * 4),
     "smc_channel_dot_f32": (c_int, [P, P, P, P, P, c_int64, c_int64, c_int, P]),
@@ -163,6 +168,29 @@ def ptr(t):
     return t.data_ptr()
 
 
+_plan_state = (0, 0)
+
+
+@contextlib.contextmanager
+def plan_batch(plan, local):
+    """Plan every batch-dependent launch decision (split-K, tile configuration, channel split) of the work enqueued
+    inside as for ``plan`` images per ``local`` images of the call (smc_set_plan_batch): a data-parallel shard of
+    ``local`` images of a ``plan``-image batch then computes each image bit for bit as the whole batch does.
+    Restores the previous setting on exit (nestable)."""
+    global _plan_state
+    prev = _plan_state
+    new = (0, 0) if not plan or not local or plan == local else (int(plan), int(local))
+    if new != prev:
+        call("smc_set_plan_batch", *new)
+        _plan_state = new
+    try:
+        yield
+    finally:
+        if _plan_state != prev:
+            call("smc_set_plan_batch", *prev)
+            _plan_state = prev
+
+
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
@@ -188,8 +216,9 @@ class KernelTimer:
         s.record()
         return s, e, flops, nbytes, kind, flops if equiv_flops is None else equiv_flops
 
-    def finish(self, token):
-        s, e, flops, nbytes, kind, eq = token
+    def finish(self, token, kind=None):
+        s, e, flops, nbytes, kind0, eq = token
+        kind = kind0 if kind is None else kind
         e.record()
         self.records.append((s, e, flops, nbytes, kind, eq))
 

@@ -22,7 +22,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import clip_model, synthetic, vit_hip
+from . import clip_model, rowops, synthetic, vit_hip
 
 MODEL_NAMES = {"small": "ViT-B/32", "large": "ViT-B/16"}
 
@@ -39,6 +39,10 @@ class _DirectionHead(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, e, src, t):
+        if e.is_cuda:   # one gfx950 launch, rows reduced in a fixed order (batch-invariant, rowops)
+            loss, gf = rowops.direction_head(e, src, t)
+            ctx.save_for_backward(gf)
+            return loss
         f = e - src
         nf = f.norm(dim=1, keepdim=True)
         u = f / nf

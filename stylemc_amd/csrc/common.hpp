@@ -20,6 +20,11 @@ int64_t conv_gemm_aux_workspace_size(int n, int cin, int cout, int y_h, int y_w,
                                      int nphases);
 int check_launch(const char* what);
 int device_cu_count();
+// Planning batch (smc_set_plan_batch): every launch decision that depends on the batch -- split-K factors, tile
+// configurations, channel splits, all of which change a result's fp32 summation order -- is made for
+// plan_batch(n) images (plan_rows(m) rows of a token-major GEMM) instead of the call's own n.  Default: n itself.
+int plan_batch(int n);
+int64_t plan_rows(int64_t m);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

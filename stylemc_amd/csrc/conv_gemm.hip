@@ -1708,7 +1708,7 @@ ConvTCfg convt_cfg(int cout) {
 
 int plan_split_convt(int n, int cin, int cout, int in_h, int in_w) {
     const ConvTCfg c = convt_cfg(cout);
-    const int64_t M = (int64_t)n * (in_h + 1) * (in_w + 1);
+    const int64_t M = (int64_t)smc::plan_batch(n) * (in_h + 1) * (in_w + 1);
     const int64_t blocks = smc::ceil_div(M, c.bm) * smc::ceil_div(cout, c.bo);
     const int ks = 4 * (cin / BK);
     const int64_t target = 2LL * smc::device_cu_count();
@@ -1744,6 +1744,7 @@ bool convt_lds_plan(int n, int cin, int cout, int in_h, int in_w, int y_h, int y
 }
 
 int plan_split_convt_lds(int n, int cin, int cout, int in_h, int in_w, const ConvTL& c, bool per_sample) {
+    n = smc::plan_batch(n);
     const int64_t hw_g = (int64_t)(in_h + 1) * (in_w + 1);
     const int64_t mt = per_sample ? n * smc::ceil_div(hw_g, c.bm) : smc::ceil_div(n * hw_g, c.bm);
     const int64_t blocks = mt * (cout / c.bo);
@@ -1775,7 +1776,7 @@ int plan_split(int n, int cin, int cout, const smc_conv_phase* ph, int nph, cons
     int64_t blocks = 0;
     int min_ks = 1 << 30;
     for (int i = 0; i < nph; ++i) {
-        const int64_t M = (int64_t)n * ph[i].out_h * ph[i].out_w;
+        const int64_t M = (int64_t)smc::plan_batch(n) * ph[i].out_h * ph[i].out_w;
         blocks += smc::ceil_div(M, c.bm) * smc::ceil_div(cout, c.bo);
         const int ks = ph[i].ntaps * (cin / BK);
         if (ks < min_ks) min_ks = ks;
@@ -1850,7 +1851,8 @@ bool small_tile_ok(int n, int cin, int cout, int in_h, int in_w, const smc_conv_
     int64_t blocks = 0;
     int taps_all = 0;
     for (int i = 0; i < nph; ++i) {
-        blocks += smc::ceil_div((int64_t)n * ph[i].out_h * ph[i].out_w, base.bm) * smc::ceil_div(cout, base.bo);
+        blocks += smc::ceil_div((int64_t)smc::plan_batch(n) * ph[i].out_h * ph[i].out_w, base.bm) *
+                  smc::ceil_div(cout, base.bo);
         taps_all += ph[i].ntaps;
     }
     // threshold measured on the FFHQ-1024 / IR-SE50 shapes (tools/bench_gemm.py, tools/prof_irse.py): the
@@ -1953,9 +1955,13 @@ SMC_API int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, 
 
 namespace {
 
+// whether the last conv_gemm_impl call of this thread launched split-bf16 products (smc_conv_gemm_last_x3)
+thread_local int g_last_x3 = 0;
+
 int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y, int cout, int y_h, int y_w,
                    const smc_conv_phase* phases, int nphases, const float* s_in, const smc_conv_epilogue* epi,
                    float* workspace, int64_t workspace_bytes, void* stream, int tag) {
+    g_last_x3 = 0;
     int rc = validate(x, n, cin, in_h, in_w, y, cout, y_h, y_w, phases, nphases);
     if (rc != SMC_OK) return rc;
     Cfg c;
@@ -2080,6 +2086,7 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         p.per_sample = t_per_sample ? 1 : 0;
         p.ntn = cout / tl.bo;
         dim3 g((unsigned)(mt * p.ntn), 1, (unsigned)nsplit);
+        g_last_x3 = x3 ? 1 : 0;
         if (x3 && tl.id == 1) hipLaunchKernelGGL((convt_x3_kernel<2, 2, 1, 2>), g, dim3(NT), 0, st, p, ctt);
         else if (x3) hipLaunchKernelGGL((convt_x3_kernel<1, 4, 1, 1>), g, dim3(NT), 0, st, p, ctt);
         else if (tl.id == 1) hipLaunchKernelGGL((convt_lds_kernel<2, 2, 1, 2, 16>), g, dim3(NT), 0, st, p, ctt);
@@ -2133,6 +2140,7 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             const bool k32 = cfg == 0 && cin % 32 == 0;
             // 32-channel K steps for the narrow tiles too (A/B knob SMC_X3_K32_SMALL: half the barriers per FLOP)
             const bool k32s = SMC_X3_K32_SMALL && cin % 32 == 0;
+            g_last_x3 = 1;
             if (cfg == 0 && k32 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0 && k32) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 16, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
@@ -2210,6 +2218,8 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
 }
 
 }  // namespace
+
+SMC_API int smc_conv_gemm_last_x3(void) { return g_last_x3; }
 
 SMC_API int64_t smc_conv_weights_x3_bytes(int ntaps, int cin, int cout) {
     if (ntaps < 1 || ntaps > 9 || cin < 16 || cin % 16 || cout < 1) return 0;

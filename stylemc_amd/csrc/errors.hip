@@ -1,4 +1,5 @@
 // Error state and device queries for the C ABI.
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -41,7 +42,28 @@ int device_cu_count() {
     return cached_cus;
 }
 
+// (plan, local) packed into one word: process-wide (the autograd engine runs backward calls on its own thread), set
+// by the host thread that enqueues a step before it enqueues it
+static std::atomic<int64_t> g_plan{0};
+
+int64_t plan_rows(int64_t m) {
+    const int64_t v = g_plan.load(std::memory_order_relaxed);
+    const int64_t plan = v >> 32, local = v & 0xffffffff;
+    if (plan <= 0 || local <= 0 || plan == local) return m;
+    const int64_t r = (m * plan + local / 2) / local;
+    return r < 1 ? 1 : r;
+}
+
+int plan_batch(int n) { return (int)plan_rows(n); }
+
 }  // namespace smc
+
+SMC_API int smc_set_plan_batch(int plan, int local) {
+    SMC_CHECK(plan >= 0 && local >= 0 && (plan == 0) == (local == 0), "smc_set_plan_batch: bad arguments (%d, %d)",
+              plan, local);
+    smc::g_plan.store(((int64_t)plan << 32) | (int64_t)local, std::memory_order_relaxed);
+    return SMC_OK;
+}
 
 SMC_API int smc_abi_version(void) { return SMC_ABI_VERSION; }
 

@@ -386,7 +386,8 @@ SMC_API int smc_torgb_act_bwd_f32(const float* g_rgb, const float* y_rgb, const 
     // a small position grid (the 128..512-px blocks) also splits the channels over grid.z, in whole chunks, until the
     // launch holds ~4 workgroups per CU (r = 128: 64 workgroups walking 256 channels took 264 us).
     int nz = 1;
-    while ((int64_t)grid.x * grid.y * nz < 4 * (int64_t)smc::device_cu_count() && cin % (16 * nz) == 0) nz *= 2;
+    const int64_t plan_wg = (int64_t)grid.x * smc::plan_batch(n);   // grid.y = n: the split from the planning batch
+    while (plan_wg * nz < 4 * (int64_t)smc::device_cu_count() && cin % (16 * nz) == 0) nz *= 2;
     grid.z = (unsigned)nz;
     const int kch = cin / nz;
     if (vec)

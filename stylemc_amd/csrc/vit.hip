@@ -206,7 +206,7 @@ __global__ void lin_splitk_epilogue_kernel(const float* ws, int nsplit, float* c
 // plus one step for the partial-tile reduction when s > 1.  (M = 200: the 2304-wide QKV product picks
 // s = 2 -> 252 workgroups, the 768-wide projections s = 6 -> 252, the 3072-wide MLP product s = 3.)
 int lin_nsplit(int M, int N, int K) {
-    const int64_t tiles = smc::ceil_div(M, LBM) * smc::ceil_div(N, LBN);
+    const int64_t tiles = smc::ceil_div(smc::plan_rows(M), LBM) * smc::ceil_div(N, LBN);
     const int nks = K / LBK;
     const int64_t cus = smc::device_cu_count();
     int best = 1;
@@ -666,7 +666,7 @@ bool lin_v2_ok(int N, int K, int lda, int ldb) {
 }
 
 int lin_nsplit2(int M, int N, int K) {
-    const int64_t tiles = smc::ceil_div(M, L2M) * (N / L2N);
+    const int64_t tiles = smc::ceil_div(smc::plan_rows(M), L2M) * (N / L2N);
     const int nks = K / L2K;
     const int64_t cus = smc::device_cu_count();
     int best = 1;

@@ -541,7 +541,7 @@ constexpr int64_t kWinoSplitTarget = SMC_WINO_SPLIT_TARGET;
 int wino_nsplit(int n, int cin, int cout, int h, int w) {
     const int tc = wino_tc(h, w);
     if (!tc) return 1;
-    const int64_t items = (int64_t)n * ((w / 2) / tc) * ((h / 2) / (WBT / tc)) * (cout / WBO);
+    const int64_t items = (int64_t)smc::plan_batch(n) * ((w / 2) / tc) * ((h / 2) / (WBT / tc)) * (cout / WBO);
     const int nsteps = cin / WBK;
     int ns = 1;
     while (items * ns < kWinoSplitTarget && nsteps % (2 * ns) == 0 && nsteps / (2 * ns) >= 8) ns *= 2;

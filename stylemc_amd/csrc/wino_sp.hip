@@ -285,7 +285,8 @@ SpPlan sp_plan(int n, int cin, int cout, int h, int w) {
     // split-K reduction grows with the splits), whole 8-channel steps per split, at most SMAXK of them
     const int target = SP_WG_PER_CU * smc::device_cu_count();
     const int nst = cin / SBK;
-    s.nsplit = std::min(nst, std::max((int)smc::ceil_div(nst, SMAXK), (int)smc::ceil_div(target, s.nitems)));
+    const int plan_items = ((smc::plan_batch(n) + s.ipi - 1) / s.ipi) * s.ntn;   // the split from the planning batch
+    s.nsplit = std::min(nst, std::max((int)smc::ceil_div(nst, SMAXK), (int)smc::ceil_div(target, plan_items)));
     return s;
 }
 

@@ -2,9 +2,12 @@
 
 find_direction shards naturally: the seeds of a batch are independent images.  Every rank holds the
 frozen networks, the full S table and an identical direction; rank r takes a contiguous slice of the
-batch, and ONE all_reduce(SUM) per step combines the [8*512] direction gradient with the 4 loss
-scalars (16.4 KB -- latency-bound over xGMI, so one fused buffer).  The reference has no distributed
-code on this path; this is the build's single exchange step (section 8(e)).
+batch.  The step's single exchange (the reference has no distributed code on this
+path, section 2.3) is ONE all_gather of per-image rows -- each image's [8*512] direction gradient and its
+4 loss terms, 16.4 KB a row, 4 rows per rank at batch 4: latency-bound over xGMI either way -- after which
+every rank sums the global batch's rows in the same fixed order.  An all_reduce(SUM) would add the ranks'
+partial sums in the collective's own order (ring chunks start at different ranks), so its result would
+depend on the number of ranks; the gathered rows make the N-rank direction equal the 1-rank one bit for bit.
 """
 import os
 
@@ -32,6 +35,24 @@ class World:
         if self.distributed:
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t
+
+    def gather_rows(self, rows, lo, hi):
+        """Every rank's rows of the global batch [lo, hi) (rank r holds shard_rows(lo, hi, r, N)) as one contiguous
+        [hi - lo, F] tensor in global order, on every rank.  One all_gather of equal-size blocks (shards differ by at
+        most one row: zero-padded).  Gloo has no device-tensor all_gather on every build: its rows go by the host."""
+        if not self.distributed:
+            return rows.contiguous()
+        N = self.world_size
+        cap = -(-(hi - lo) // N)
+        feat = rows.shape[1]
+        dev = rows.device
+        host = self.backend != "nccl" and rows.is_cuda
+        block = torch.zeros(cap, feat, dtype=rows.dtype, device="cpu" if host else dev)
+        block[:rows.shape[0]] = rows.cpu() if host else rows
+        parts = [torch.empty_like(block) for _ in range(N)]
+        dist.all_gather(parts, block)
+        out = torch.cat([parts[r][:b - a] for r, (a, b) in ((r, shard_rows(lo, hi, r, N)) for r in range(N))])
+        return out.to(dev) if host else out
 
     def all_max(self, v, device):
         if not self.distributed:

@@ -19,6 +19,7 @@ generate_image is called with the missing ``device`` fixed (:309,312 raise TypeE
 Multi-GPU: every rank draws the same i, takes its contiguous slice of the global batch, and one
 all_reduce(SUM) per step combines the gradient and the loss terms (stylemc_amd.dist).
 """
+import contextlib
 import math
 import os
 import time
@@ -28,8 +29,9 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import _hip
 from . import dist as _dist
-from . import utils
+from . import rowops, utils
 
 N_STYLE_CHANNELS = utils.N_STYLE_CHANNELS
 S_TRAINABLE_SPACE_CHANNELS = utils.S_TRAINABLE_SPACE_CHANNELS
@@ -168,7 +170,7 @@ class DirectionFinder:
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
                  overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None, G2=None, temp_shapes2=None,
-                 prefetch_id=True):
+                 prefetch_id=True, plan_batch=None):
         self.G = G
         # the edited image's generator (train_latent_mapper.py:100-106,159-162 --network2; default G itself)
         self.G_edit = G2 if G2 is not None else G
@@ -201,6 +203,11 @@ class DirectionFinder:
         self.id_loss = id_loss
         self.until_k = RESOLUTION_DICT.get(resolution, int(math.log2(resolution)) - 2)
         self.B = int(global_batch or batch_size)
+        # batch-invariant kernel plans: every launch of a step is planned as for `plan_batch` images (default: the
+        # per-rank batch_size) whatever this rank's shard holds, so a shard computes each image's gradient row bit
+        # for bit as the whole batch does in one process (smc_set_plan_batch); the rows are then summed in one
+        # fixed order over the global batch (combine) -- the N-rank direction equals the 1-rank one exactly
+        self.plan_batch = int(plan_batch or batch_size)
         self.lr0 = learning_rate
         self.n_epochs = n_epochs
         self.coef = dict(id=identity_loss_coef, l2=l2_reg_coef, clip=clip_loss_coef)
@@ -326,17 +333,20 @@ class DirectionFinder:
         return id_terms, clip_terms
 
     def _local_terms(self, styles, denom, key=None, d=None):
-        """Sum-form loss of this rank's shard: every per-sample term / global batch size.  Returns the gradient
-        w.r.t. ``d`` (default: a leaf copy of the shared direction) and the 4 loss terms.
+        """Sum-form loss of this rank's shard: every per-sample term / global batch size.  With ``d`` given (the
+        latent mapper's per-sample delta): the gradient w.r.t. ``d`` and the 4 summed loss terms.  Without: the
+        shard's per-image rows [n, 8*512 + 4] -- image i's gradient w.r.t. the shared direction (the direction
+        enters as a per-image leaf, so autograd does not sum over the batch) and its 4 loss terms.
 
         On the GPU the original-image branch runs on a second HIP stream, concurrently with the edited
         image's synthesis (it shares no data with it), and joins before the losses.
         """
-        if d is None:
-            d = self.delta.detach().clone().requires_grad_(True)
+        per_image = d is None
+        if per_image:
+            d = self.delta.detach().expand(styles.shape[0], -1, -1).clone().requires_grad_(True)
         if self.batch_losses:
             id_terms, clip_terms = self._pair_terms(styles, d, key)
-            return self._finish(styles, d, id_terms, clip_terms, denom)
+            return self._finish(styles, d, id_terms, clip_terms, denom, per_image)
         side = self._side_stream()
         if side is not None:
             main = torch.cuda.current_stream()
@@ -354,11 +364,26 @@ class DirectionFinder:
         id_terms = self.id_loss.per_sample_with(img, y_feats)
         clip_terms = sum(w * cl.per_sample_with(e, t) for (cl, w), e, (t, _) in
                          zip(self.clip_losses, src_embs, self._clip_inputs(img, None)))
-        return self._finish(styles, d, id_terms, clip_terms, denom)
+        return self._finish(styles, d, id_terms, clip_terms, denom, per_image)
 
-    def _finish(self, styles, d, id_terms, clip_terms, denom):
+    def _finish(self, styles, d, id_terms, clip_terms, denom, per_image=False):
         T = S_TRAINABLE_SPACE_CHANNELS
         sT = styles.index_select(1, self.t_idx)
+        if per_image:
+            l2_den = float(denom * len(T) * 512)
+            if FUSED_TOTAL:
+                total, _ = _LossTotal.apply(id_terms, clip_terms, d, sT, self.coef["id"], self.coef["clip"],
+                                            self.coef["l2"], l2_den, float(denom))
+            else:
+                total = (self.coef["id"] * id_terms.sum() / denom + self.coef["clip"] * clip_terms.sum() / denom +
+                         self.coef["l2"] * ((sT + d) - sT).square().sum() / l2_den)
+            (g,) = torch.autograd.grad(total, d)
+            with torch.no_grad():   # each image's share of the 4 logged terms (sum form)
+                diff = ((sT + d) - sT).flatten(1)
+                l2 = rowops.row_dot(diff, diff)
+                parts = torch.stack([self.coef["clip"] * clip_terms / denom, self.coef["id"] * id_terms / denom,
+                                     torch.zeros_like(l2), self.coef["l2"] * l2 / l2_den], 1)
+            return torch.cat([g.flatten(1), parts.to(g.dtype)], 1)
         if FUSED_TOTAL:
             total, parts = _LossTotal.apply(id_terms, clip_terms, d, sT, self.coef["id"], self.coef["clip"],
                                             self.coef["l2"], float(denom * len(T) * 512), float(denom))
@@ -382,6 +407,12 @@ class DirectionFinder:
         lo, hi = i * self.B, min((i + 1) * self.B, self.n_items)
         return lo, hi, _dist.shard_rows(lo, hi, self.world.rank, self.world.world_size)
 
+    def _plan(self, n_local):
+        """The kernel-plan scope of a shard of n_local images (see plan_batch)."""
+        if self.device.type != "cuda":
+            return contextlib.nullcontext()
+        return _hip.plan_batch(self.plan_batch, n_local)
+
     def _prefetch_next(self):
         """Draw the next iteration's batch (the same single randint per iteration, one step early) and start
         its original-image synthesis on the third stream once this iteration's forward is done."""
@@ -392,7 +423,7 @@ class DirectionFinder:
         if getattr(self, "_pre", None) is None:
             self._pre = self.stream_factory(self.device)
         self._pre.wait_event(self._fwd_done)
-        with torch.cuda.stream(self._pre), torch.no_grad():
+        with torch.cuda.stream(self._pre), torch.no_grad(), self._plan(b - a):
             out = self._prefetch_body(self.styles_array[a:b])
         self._pref = ((a, b),) + out
 
@@ -402,14 +433,14 @@ class DirectionFinder:
         return orig, feats, None
 
     def step(self):
-        """One iteration: this rank's shard terms (local_step), the all_reduce, the SGD update (apply_step)."""
-        buf = self.local_step()
-        self.world.all_reduce_(buf)
-        return self.apply_step(buf)
+        """One iteration: this rank's per-image rows (local_step), the exchange + fixed-order sum (combine), the
+        SGD update (apply_step)."""
+        return self.apply_step(self.combine(self.local_step()))
 
     def local_step(self):
-        """This rank's part of an iteration: the batch pick, the shard's sum-form gradient and loss terms in one
-        fused [8*512 + 4] buffer (zeros for an empty shard), the next batch's prefetch."""
+        """This rank's part of an iteration: the batch pick, one [8*512 + 4] row per image of its shard (the
+        image's sum-form direction gradient and loss terms; [0, 8*512 + 4] for an empty shard), the next batch's
+        prefetch."""
         self.it += 1
         if self._next_i is not None:
             i, self._next_i = self._next_i, None
@@ -417,18 +448,26 @@ class DirectionFinder:
             i = self.rng.randint(0, self.num_batches)
         self._cur_i = i
         lo, hi, (a, b) = self._shard(i)
+        self._cur_span = (lo, hi)
         self.styles_direction.index_copy_(1, self.t_idx, self.delta)
-        buf = torch.zeros(self.delta.numel() + 4, device=self.device)
         pipelined = self.prefetch_orig and self.batch_losses and self._side_stream() is not None
         if b > a:
-            g, parts = self._local_terms(self.styles_array[a:b], hi - lo, key=(a, b))
-            buf[:-4] = g.flatten()
-            buf[-4:] = parts
+            with self._plan(b - a):
+                rows = self._local_terms(self.styles_array[a:b], hi - lo, key=(a, b))
             if pipelined:
                 self._prefetch_next()
-        elif pipelined:
-            self._pref = None
-        return buf
+        else:
+            rows = torch.zeros(0, self.delta.numel() + 4, device=self.device)
+            if pipelined:
+                self._pref = None
+        return rows
+
+    def combine(self, rows):
+        """The iteration's [8*512 + 4] buffer from every rank's per-image rows: gathered in global image order
+        (World.gather_rows; one rank: the rows themselves) and summed over the global batch in one fixed order --
+        the same tensor and the same reduction whatever the number of ranks."""
+        lo, hi = self._cur_span
+        return self.world.gather_rows(rows, lo, hi).sum(0)
 
     def apply_step(self, buf):
         """The SGD update from the reduced buffer (every rank holds the same one after the all_reduce)."""

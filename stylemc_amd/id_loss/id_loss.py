@@ -11,6 +11,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .. import rowops
 from .model_irse import build_irse50
 
 
@@ -91,7 +92,7 @@ class IDLoss(nn.Module):
             b = self.face_crop(y)
         x = torch.cat([a, b])
         f = self.facenet(x, n_grad=n) if getattr(self.facenet, "supports_partial_grad", False) else self.facenet(x)
-        return 1 - (f[:n] * f[n:].detach()).sum(dim=1)
+        return 1 - rowops.dot(f[:n], f[n:].detach())
 
     @torch.no_grad()
     def target_feats(self, y):
@@ -99,7 +100,7 @@ class IDLoss(nn.Module):
         return self.extract_feats(y)
 
     def per_sample_with(self, y_hat, y_feats):
-        return 1 - (self.extract_feats(y_hat) * y_feats).sum(dim=1)
+        return 1 - rowops.dot(self.extract_feats(y_hat), y_feats)
 
     def per_sample(self, y_hat, y):
         """(1 - <f(y_hat_i), f(y_i)>) for each i; y's features are detached."""

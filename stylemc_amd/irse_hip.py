@@ -14,7 +14,7 @@ import ctypes
 import torch
 from torch import nn
 
-from . import _hip
+from . import _hip, rowops
 from .id_loss.model_irse import Backbone
 from . import modconv
 from .modconv import _phase
@@ -95,7 +95,7 @@ class _Packed:
         def phase(taps, stride, oh, ow, wk, oy=0, ox=0, sy=1, sx=1):
             wk = d(wk)
             # split-bf16 planes for the direct GEMMs (X3 below; kept alive with the packed weights)
-            wx = modconv.x3_planes(wk, wk.shape[1], wk.shape[2]) if X3 else None
+            wx = modconv.x3_planes(wk, wk.shape[1], wk.shape[2], enabled=X3)
             if wx is not None:
                 self.keep.append(wx)
             return _phase(taps, stride, oh, ow, oy, ox, sy, sx, wk, wx)
@@ -298,7 +298,7 @@ class HipIRSE50(nn.Module):
     def forward(self, x, n_grad=None):
         """n_grad: back-propagate only the leading n_grad faces (the rest get a zero gradient)."""
         f = _IrseFn.apply(x, self, n_grad)
-        return f / torch.norm(f, 2, 1, True)   # model_irse.py:48 l2_norm
+        return rowops.l2_normalize(f)          # model_irse.py:48 l2_norm (rows in a fixed order)
 
 
 def build_irse50(state_dict=None, seed=3, device="cuda"):

@@ -43,10 +43,11 @@ def _phase(taps, in_stride, out_h, out_w, out_oy, out_ox, out_sy, out_sx, wk, wk
 X3 = True
 
 
-def x3_planes(wk, cin, cout):
+def x3_planes(wk, cin, cout, enabled=None):
     """The split-bf16 planes (smc_conv_weights_x3) of [ntaps][cin][cout] GEMM weights, or None where the kernel has
-    no split form (cin % 16) or the weights are not on the GPU."""
-    if not (X3 and wk.is_cuda):
+    no split form (cin % 16), the weights are not on the GPU or split products are off (``enabled``; default: this
+    module's X3 -- the IR-SE50 executor passes its own switch)."""
+    if not ((X3 if enabled is None else enabled) and wk.is_cuda):
         return None
     lib = _hip.load()
     nb = lib.smc_conv_weights_x3_bytes(wk.shape[0], cin, cout)
@@ -84,13 +85,36 @@ class PackedConv:
                     wk = torch.stack([W[:, :, ky, kx].t() for ky, kx in sel]).contiguous()  # [t][i][o]
                     self.phases.append((py, px, [(-(ky - py) // 2, -(kx - px) // 2) for ky, kx in sel], wk))
             self.bwd_taps = [(ky, kx) for ky, kx in taps]  # stride-2 gather over dT
-        # split-bf16 planes of the direct GEMMs' weights (the caller -- LayerSpec -- waits for the packing kernels)
-        self.x3_fwd = x3_planes(self.wk_fwd, self.cin, self.cout) if up == 1 else None
-        self.x3_bwd = x3_planes(self.wk_bwd, self.cout, self.cin)
-        self.x3_phases = [x3_planes(wk, self.cin, self.cout) for _, _, _, wk in self.phases] if up == 2 else None
+        # split-bf16 planes of the direct GEMMs' weights, built on first use (x3_fwd / x3_bwd / x3_phases): a layer
+        # whose forward or data gradient always takes a Winograd kernel never builds (1.5x the fp32 bytes of) that
+        # direction's planes.  The switch is read once, here.
+        self.use_x3 = X3
+        self._x3 = {}
         self._cache = {}
         self._wino = {}
         self._wino4 = {}
+
+    def _planes(self, key, wk, cin, cout):
+        if key not in self._x3:
+            p = x3_planes(wk, cin, cout, enabled=self.use_x3)
+            if p is not None:   # built on this stream, read from any: wait once (first use, i.e. a warm-up step)
+                torch.cuda.current_stream(wk.device).synchronize()
+            self._x3[key] = p
+        return self._x3[key]
+
+    @property
+    def x3_fwd(self):
+        return self._planes("f", self.wk_fwd, self.cin, self.cout) if self.up == 1 else None
+
+    @property
+    def x3_bwd(self):
+        return self._planes("b", self.wk_bwd, self.cout, self.cin)
+
+    @property
+    def x3_phases(self):
+        if self.up != 2:
+            return None
+        return [self._planes(("p", i), wk, self.cin, self.cout) for i, (_, _, _, wk) in enumerate(self.phases)]
 
     def wino_weights(self, flip):
         """Winograd F(2x2, 3x3) transformed taps (smc_wino_weights_f32) of the 3x3 'same' conv, built once on the
@@ -154,12 +178,12 @@ def gemm(x, y, phases, nph, cin, cout, s=None, epi=None, alg_flops=0.0, alg_byte
     ws_bytes = lib.smc_conv_gemm_workspace_size(n, cin, cout, yh, yw, phases, nph)
     ws = torch.empty(max(ws_bytes // 4, 1), device=x.device, dtype=torch.float32) if ws_bytes > 0 else None
     tm = _hip.timer()
-    kind = "direct_x3" if all(phases[i].wk_x3 for i in range(nph)) else "direct"
-    tok = tm.wrap(alg_flops, alg_bytes, kind=kind) if tm is not None else None
+    tok = tm.wrap(alg_flops, alg_bytes, kind="direct") if tm is not None else None
     _hip.call("smc_conv_gemm_f32", x.data_ptr(), n, cin, ih, iw, y.data_ptr(), cout, yh, yw, phases, nph,
               _hip.ptr(s), ctypes.byref(epi) if epi is not None else None, _hip.ptr(ws), ws_bytes, _hip.stream())
     if tok is not None:
-        tm.finish(tok)
+        # the product form the library actually launched (split-bf16 only where the LDS-DMA kernels took the call)
+        tm.finish(tok, kind="direct_x3" if lib.smc_conv_gemm_last_x3() else "direct")
 
 
 # Winograd F(2x2, 3x3) for the 3x3 stride-1 convs wherever smc_conv3x3_wino_supported() has a kernel (module

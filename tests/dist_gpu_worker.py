@@ -70,9 +70,8 @@ def run_cases(world, dev, G, clip, idl, shapes):
 
 def run_cases_simulated(dev, G, clip, idl, shapes, world_size=2):
     """The N-rank run replayed in ONE process: a finder per rank view (World(rank=r, world_size=N)), in lockstep --
-    each computes its shard's buffer (local_step), the buffers are summed (what all_reduce(SUM) of N = 2 computes,
-    one fp32 add per element), every view applies the sum (apply_step).  Same kernels on the same shard sizes as the
-    real ranks, so the real run must match it bit for bit."""
+    each computes its shard's per-image rows (local_step, under its own plan scope), the rows are concatenated in rank
+    order (what the all_gather assembles), every view applies their fixed-order sum (apply_step)."""
     from stylemc_amd import dist as sdist
     out = {}
     for gb, n_items, steps in CASES:
@@ -80,11 +79,9 @@ def run_cases_simulated(dev, G, clip, idl, shapes, world_size=2):
               for r in range(world_size)]
         parts, picks = [], []
         for _ in range(steps):
-            bufs = [f.local_step() for f in fs]
-            tot = bufs[0]
-            for b in bufs[1:]:
-                tot = tot + b
-            lasts = [f.apply_step(tot.clone()) for f in fs]
+            rows = torch.cat([f.local_step() for f in fs])
+            buf = rows.sum(0)
+            lasts = [f.apply_step(buf.clone()) for f in fs]
             parts.append(lasts[0]["parts"].cpu())
             picks.append(lasts[0]["batch"])
         for f in fs[1:]:

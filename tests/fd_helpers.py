@@ -49,6 +49,32 @@ def oracle_rows_synth(G, until_k, styles, temp_shapes, noise_mode="const", delta
     return img
 
 
+def per_image_synth(G, until_k, styles, temp_shapes, noise_mode="const", delta=None,
+                    trainable=S_TRAINABLE_SPACE_CHANNELS):
+    """oracle_rows_synth one image at a time: each image's result (and gradient) is then independent of the batch
+    it came in -- CPU torch picks conv / matmul algorithms by batch size, so a batched oracle is not."""
+    outs = []
+    for i in range(styles.shape[0]):
+        d = None if delta is None else (delta[i:i + 1] if delta.shape[0] > 1 else delta)
+        outs.append(oracle_rows_synth(G, until_k, styles[i:i + 1], temp_shapes, noise_mode, delta=d,
+                                      trainable=trainable))
+    return torch.cat(outs)
+
+
+class _PerImage(torch.nn.Module):
+    def __init__(self, inner):
+        super().__init__()
+        self.inner = inner
+
+    def forward(self, x):
+        return torch.cat([self.inner(x[i:i + 1]) for i in range(x.shape[0])])
+
+
+def per_image_module(m):
+    """A batch-invariant wrapper: the module applied image by image (see per_image_synth)."""
+    return _PerImage(m)
+
+
 class OracleID(torch.nn.Module):
     def __init__(self, facenet):
         super().__init__()

@@ -5,14 +5,12 @@ RCCL two ranks) run DirectionFinder with the default schedule -- the next iterat
 early, its original image prefetched on the third stream, empty-shard ranks skipping the prefetch -- at global
 batch 4 (2 + 2), 3 (2 + 1, and a short last batch of 1 that empties rank 1) and 1 (rank 1 empty every step).
 
-Checks:
-  * bit for bit against the same two rank views replayed in this process in lockstep (local_step on each view,
-    the two buffers summed -- all_reduce(SUM) of two ranks is one fp32 add per element -- apply_step on each): the
-    multi-process run, its prefetch pipeline and the exchange add nothing beyond that sum;
-  * against the single-rank run of the same global batches: same batch picks; loss terms rtol 1e-3, update
-    cosine >= 0.9999 and max-norm relative error <= 1e-2 -- shards of 2 images run other kernel plans (split-K
-    factors chosen per grid) than the 4-image batch, and the directional CLIP term amplifies those fp32 rounding
-    differences step over step (tests/test_gpu_find_direction.py's tolerances, same reason).
+Every launch of a shard is planned for the full batch (smc_set_plan_batch: split-K factors, tile configurations and
+channel splits from the planning batch, not the shard), the loss heads reduce rows in a fixed order (rowops), each
+image's gradient row comes back separately and the global batch's rows are summed in one fixed order after the
+all_gather.  So the two-rank run must equal, BIT FOR BIT:
+  * the single-rank run of the same global batches (deltas, saved directions, loss terms, batch picks);
+  * the same two rank views replayed in this process in lockstep.
 """
 import os
 import socket
@@ -72,16 +70,10 @@ def test_two_ranks_pipelined_match_single_rank(tmp_path):
     sim = W.run_cases_simulated(dev, *prob)
     ref = W.run_cases(sdist.World(), dev, *prob)
     from stylemc_amd.find_direction import initial_delta
-    init = initial_delta(0, 0.01).numpy().astype(np.float64).ravel()
     for gb, _, steps in W.CASES:
         assert np.isfinite(got[f"delta_{gb}"]).all()
+        init = initial_delta(0, 0.01).numpy().reshape(got[f"delta_{gb}"].shape)
+        assert not np.array_equal(got[f"delta_{gb}"], init), gb
         for key in ("picks", "delta", "sdir", "parts"):
-            assert np.array_equal(got[f"{key}_{gb}"], sim[f"{key}_{gb}"]), (gb, key)
-        assert np.array_equal(got[f"picks_{gb}"], ref[f"picks_{gb}"]), gb
-        np.testing.assert_allclose(got[f"parts_{gb}"], ref[f"parts_{gb}"], rtol=1e-3, atol=1e-5)
-        a = got[f"delta_{gb}"].astype(np.float64).ravel() - init
-        b = ref[f"delta_{gb}"].astype(np.float64).ravel() - init
-        cos = float(a @ b / np.linalg.norm(a) / np.linalg.norm(b))
-        assert cos >= 0.9999, (gb, cos)
-        err = float(np.abs(got[f"delta_{gb}"] - ref[f"delta_{gb}"]).max() / np.abs(ref[f"delta_{gb}"]).max())
-        assert err <= 1e-2, (gb, err)
+            assert np.array_equal(got[f"{key}_{gb}"], sim[f"{key}_{gb}"]), (gb, key, "vs lockstep replay")
+            assert np.array_equal(got[f"{key}_{gb}"], ref[f"{key}_{gb}"]), (gb, key, "vs the 1-rank run")
