@@ -208,7 +208,10 @@ def direction_parity(G, clip, id_loss, resolution, batch, iters, delta_ref, dev,
 
 def dist_selfcheck(G, clip, id_loss, world, dev, temp_shapes, resolution, batch, steps=2):
     """N > 1: the N-rank direction after `steps` steps on one global batch vs rank 0 re-running the same global
-    batch in a single process (the all_reduce must reproduce the single-process gradient)."""
+    batch in a single process.  Kernel plans are made for the global batch on every rank (plan_batch) and the
+    per-image rows are summed in one fixed order, so the two are expected bit-equal (dir_equal_1rank) -- except where
+    the single-process batch crosses a shape limit the shards do not (inputs >= 2 GiB take the register-staged
+    kernels: batch 32 at r = 1024)."""
     from stylemc_amd import dist as sdist
     from stylemc_amd import synthetic
     from stylemc_amd.find_direction import DirectionFinder, initial_delta
@@ -228,7 +231,9 @@ def dist_selfcheck(G, clip, id_loss, world, dev, temp_shapes, resolution, batch,
             f1.step()
         d_1 = f1.delta.detach().cpu().double().flatten()
         i0 = init.double().flatten()
-        out = {"dir_cosine_vs_1rank": round(torch.nn.functional.cosine_similarity(d_n, d_1, dim=0).item(), 7),
+        out = {"dir_equal_1rank": bool(torch.equal(d_n, d_1)),
+               "dir_max_abs_diff_vs_1rank": float((d_n - d_1).abs().max()),
+               "dir_cosine_vs_1rank": round(torch.nn.functional.cosine_similarity(d_n, d_1, dim=0).item(), 7),
                "update_cosine_vs_1rank": round(torch.nn.functional.cosine_similarity(d_n - i0, d_1 - i0, dim=0).item(), 7),
                "steps": steps, "global_batch": B, "backend": world.backend,
                "world_size": torch.distributed.get_world_size()}

@@ -205,7 +205,9 @@ int smc_modconv_epilogue_f32(const float* src, int nsplit, int64_t split_stride,
  * then the modconv epilogue (u_save receives U).  T: [n, c, t_h, t_pitch] of which the first t_w columns
  * are the image (t_pitch = 0: t_w; a pitch that is a multiple of 4 -- the transposed conv's odd 2h + 1
  * width padded -- takes the 16-B load path), may be `nsplit` partial planes; y: [n, c, y_h, y_w].  Only
- * the 4x4 FIR of the [1,3,3,1] resample filter has a fused kernel; other sizes return SMC_ERR_UNSUPPORTED. */
+ * the 4x4 FIR of the [1,3,3,1] resample filter has a fused kernel; other sizes return SMC_ERR_UNSUPPORTED.
+ * f = NULL (fh = fw = 4): the built-in setup_filter([1,3,3,1]) taps as compile-time constants (bit-identical to
+ * passing that filter; the kernel then holds no taps in registers). */
 int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_stride, float* y, int n, int c, int t_h,
                              int t_w, int t_pitch, int y_h, int y_w, const float* f, int fh, int fw, int padx0,
                              int pady0, float fgain, int flip, const smc_conv_epilogue* epi, void* stream);

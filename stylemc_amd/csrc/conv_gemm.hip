@@ -687,6 +687,11 @@ __global__ __launch_bounds__(256) void x3_weights_kernel(const float* wk, const 
 #ifndef SMC_X3_K32_SMALL
 #define SMC_X3_K32_SMALL 1
 #endif
+// Tiles whose waves each own all of the tile's output channels (WO = 1: 128 x 32 or 64 x 32 per wave instead of
+// 64 x 64 / 32 x 64): a B fragment is split once per workgroup instead of once per wave pair (A/B knob)
+#ifndef SMC_X3_WO1
+#define SMC_X3_WO1 1
+#endif
 // Timing probes only (0 in the library; tools/ builds a variant with SMC_AB_DEFINES): 1 drops the input DMAs after
 // the first K step, 2 the weight DMAs after the first, 4 the register split (the fp32 bits reused as the three terms)
 #ifndef SMC_X3_PROBE
@@ -764,6 +769,18 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
     const int ay = a * ph.in_stride, bx = b * ph.in_stride;
     const short* wx = ph.wx3 + (ph.wx3_stride ? (int64_t)(m0 / hw_out) * ph.wx3_stride : 0);
     const int c16n = p.cin / 16;
+    // weight-plane DMAs through a buffer resource: each lane's byte offset within a step's planes is fixed (computed
+    // once here), the step's part is wave-uniform (soffset) -- no per-DMA 64-bit address VALU in the K loop
+    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)wx, (short)0, 0x7ffffff0, 0x00020000);
+    int woff[WIW];
+#pragma unroll
+    for (int jw = 0; jw < WIW; ++jw) {
+        int j = wave + 4 * jw;
+        if (j >= WLI) j -= WLI;  // wave-uniform
+        const int L = j * 64 + lane;
+        const int run = L / BO, o = L - run * BO;   // run = chunk * 6 + term * 2 + octet
+        woff[jw] = (run * p.cout + o0 + o) * 16;
+    }
 
     auto issue = [&](int ks, int slot) {
         const int t = ks / cpk;
@@ -782,16 +799,14 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
         }
         // weight planes: 16-B lanes over [NKC][6 = term x octet][BO] (each (term, octet) run of BO lanes contiguous
         // in global memory at (((t * cin / 16 + chunk) * 6 + run) * cout + o0 + o) * 8 bf16)
-        const int64_t wbase = ((int64_t)t * c16n + ci0 / 16) * 6;
+        const int wsoff = ((t * c16n + ci0 / 16) * 6) * p.cout * 16;
 #pragma unroll
         for (int jw = 0; jw < ((SMC_X3_PROBE & 2) && ks > ks_begin ? 0 : WIW); ++jw) {
             int j = wave + 4 * jw;
             if (j >= WLI) j -= WLI;  // wave-uniform
-            const int L = j * 64 + lane;
-            const int run = L / BO, o = L - run * BO;   // run = chunk * 6 + term * 2 + octet
-            const short* src = wx + ((wbase + run) * p.cout + o0 + o) * 8;
-            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(st + j * 1024),
-                                             16, 0, 0);
+            const int vo = woff[jw];  // (through a local: hipcc drops the kernel's host stub when the array is passed)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (__attribute__((address_space(3))) void*)(st + j * 1024), 16,
+                                                     vo, wsoff, 0, 0);
         }
     };
 
@@ -2087,7 +2102,8 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
         p.ntn = cout / tl.bo;
         dim3 g((unsigned)(mt * p.ntn), 1, (unsigned)nsplit);
         g_last_x3 = x3 ? 1 : 0;
-        if (x3 && tl.id == 1) hipLaunchKernelGGL((convt_x3_kernel<2, 2, 1, 2>), g, dim3(NT), 0, st, p, ctt);
+        if (x3 && tl.id == 1 && SMC_X3_WO1) hipLaunchKernelGGL((convt_x3_kernel<1, 4, 2, 1>), g, dim3(NT), 0, st, p, ctt);
+        else if (x3 && tl.id == 1) hipLaunchKernelGGL((convt_x3_kernel<2, 2, 1, 2>), g, dim3(NT), 0, st, p, ctt);
         else if (x3) hipLaunchKernelGGL((convt_x3_kernel<1, 4, 1, 1>), g, dim3(NT), 0, st, p, ctt);
         else if (tl.id == 1) hipLaunchKernelGGL((convt_lds_kernel<2, 2, 1, 2, 16>), g, dim3(NT), 0, st, p, ctt);
         else hipLaunchKernelGGL((convt_lds_kernel<1, 4, 1, 1, 16>), g, dim3(NT), 0, st, p, ctt);
@@ -2141,7 +2157,9 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             // 32-channel K steps for the narrow tiles too (A/B knob SMC_X3_K32_SMALL: half the barriers per FLOP)
             const bool k32s = SMC_X3_K32_SMALL && cin % 32 == 0;
             g_last_x3 = 1;
-            if (cfg == 0 && k32 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
+            if (SMC_X3_WO1 && cfg == 0 && k32 && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 4, 1, 32>), grid, dim3(NT), 0, st, p);
+            else if (SMC_X3_WO1 && cfg == 5 && k32s && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 2, 1, 32>), grid, dim3(NT), 0, st, p);
+            else if (cfg == 0 && k32 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0 && k32) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 16, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 16>), grid, dim3(NT), 0, st, p);

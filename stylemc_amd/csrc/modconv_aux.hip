@@ -229,11 +229,32 @@ __device__ __forceinline__ void fir_block_split(const float* tile, int stride, i
 
 template <int FH, int FW>
 __device__ __forceinline__ void load_taps(const float* f, int flip, float fgain, float (&tp)[FH][FW]) {
+    if (FH == 4 && FW == 4 && !f) {  // the built-in [1,3,3,1] resample filter (f = NULL): see std_taps
+        constexpr float k[4] = {1.f, 3.f, 3.f, 1.f};
+#pragma unroll
+        for (int jy = 0; jy < FH; ++jy)
+#pragma unroll
+            for (int jx = 0; jx < FW; ++jx) tp[jy][jx] = k[jy] * k[jx] * (1.f / 64.f) * fgain;
+        return;
+    }
 #pragma unroll
     for (int jy = 0; jy < FH; ++jy)
 #pragma unroll
         for (int jx = 0; jx < FW; ++jx)
             tp[jy][jx] = f[(flip ? jy : FH - 1 - jy) * FW + (flip ? jx : FW - 1 - jx)] * fgain;
+}
+
+// The synthesis' resample filter, setup_filter([1,3,3,1]) = k k^T / 64, times the conv0 FIR gain 4, as compile-time
+// constants k_i k_j / 16 (exact in fp32, equal bit for bit to the values load_taps reads and scales): the FMAs take
+// literal operands and the 16 taps need no registers (blur_act_v4: 140 -> fewer VGPRs, more waves per SIMD for a
+// memory-bound kernel).  Symmetric, so the flip does not matter.
+template <int FH, int FW>
+__device__ __forceinline__ void std_taps(float (&tp)[FH][FW]) {
+    constexpr float k[4] = {1.f, 3.f, 3.f, 1.f};
+#pragma unroll
+    for (int jy = 0; jy < FH; ++jy)
+#pragma unroll
+        for (int jx = 0; jx < FW; ++jx) tp[jy][jx] = k[jy] * k[jx] * 0.0625f;
 }
 
 // Forward conv0 epilogue: U = FIR(T) (1:1, pad (pady0, padx0)), y = epi(U); stores y and U.
@@ -342,11 +363,23 @@ __global__ __launch_bounds__(256) void blur_act_fast(const float* t, int nsplit,
 #ifndef SMC_BLUR_NT
 #define SMC_BLUR_NT 1
 #endif
+// workgroups per CU the built-in-tap FIR forward is compiled for (A/B knob; profiles/r05/fir_ab/: 4 -> 103 VGPRs, no
+// spill, r = 1024 338 us; 5 -> 96 VGPRs with a 20-B spill, 372 us; runtime taps 140 VGPRs, 3 waves per SIMD, 375 us)
+#ifndef SMC_BLUR_WGS
+#define SMC_BLUR_WGS 4
+#endif
+#ifndef SMC_BLUR_STDF
+#define SMC_BLUR_STDF 1
+#endif
+// the next row tile's loads issued before this tile's FIR and stores (A/B knob)
+#ifndef SMC_BLUR_PIPE
+#define SMC_BLUR_PIPE 1
+#endif
 template <bool NT>
 __device__ __forceinline__ void st_f2(float* p, float2 v) {
     if (NT) {
-        __builtin_nontemporal_store(v.x, p);
-        __builtin_nontemporal_store(v.y, p + 1);
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(f32x2{v.x, v.y}, reinterpret_cast<f32x2*>(p));   // one dwordx2 store
     } else {
         *reinterpret_cast<float2*>(p) = v;
     }
@@ -356,8 +389,8 @@ __device__ __forceinline__ void st_f2(float* p, float2 v) {
 // before the next layer's conv has streamed the whole plane set).  Measured (profiles/r04/blur_ab/, bit-identical y):
 // TPB 4 + NT 712 -> 650 us over the five conv0 layers; TPB 8 / 16 no better; the same on the backward lost (dT is read
 // right away by the transposed conv's data gradient).
-template <int FH, int FW, int TPB, bool NT>
-__global__ __launch_bounds__(256) void blur_act_v4(const float* t, int nsplit, int64_t split_stride, float* y, int c,
+template <int FH, int FW, int TPB, bool NT, bool STDF = false>
+__global__ __launch_bounds__(256, STDF ? SMC_BLUR_WGS : 1) void blur_act_v4(const float* t, int nsplit, int64_t split_stride, float* y, int c,
                                                    int t_h, int t_w, int tp_w, int y_h, int y_w, const float* f,
                                                    int padx0, int pady0, float fgain, int flip, Epi e) {
     constexpr int ROWS = kFH + FH - 1, COLS = kFW + FW - 1, STRIDE = COLS + 1;
@@ -369,33 +402,44 @@ __global__ __launch_bounds__(256) void blur_act_v4(const float* t, int nsplit, i
     const int64_t nc = blockIdx.z;
     const int n = (int)(nc / c), o = (int)(nc - (int64_t)n * c);
     float tp[FH][FW];
-    load_taps<FH, FW>(f, flip, fgain, tp);
+    if constexpr (STDF) std_taps<FH, FW>(tp);
+    else load_taps<FH, FW>(f, flip, fgain, tp);
     const float nstr = e.noise_strength ? *e.noise_strength : 1.f;
     const float dv = e.d ? e.d[nc] : 1.f;
     const float bv = e.bias ? e.bias[o] : 0.f;
-    for (int tb = 0; tb < TPB; ++tb) {
-        const int oy0 = (blockIdx.y * TPB + tb) * kFH;
-        if (oy0 >= y_h) break;
-        if (tb > 0) __syncthreads();  // the previous tile's FIR reads are done
-        const int iy0 = oy0 - pady0, ix0 = ox0 - padx0;
-        const int64_t pbase = nc * (int64_t)t_h * tp_w;
-        float4 v[NL];
-        int64_t off[NL];   // buffer index of the group's first element, -1: no valid element
-        int gx[NL];        // image column of the group's first element
+    const int ix0 = ox0 - padx0;
+    const int64_t pbase = nc * (int64_t)t_h * tp_w;
+    // (16-B alignment of the groups: the plane base's offset mod 4 floats; the groups are aligned in the buffer)
+    const int pmis = (int)(pbase & 3);
+    const float* tpl = t + (pbase - pmis);        // 16-B aligned; plane element e sits at tpl[e + pmis]
+    float4 v[NL];
+    int off[NL];   // plane-relative (+ pmis) index of the group's first element, -1: no valid element
+    int gx[NL];    // image column of the group's first element
+    // tile tb's haloed rows into registers (issued one tile ahead: their HBM latency runs under the previous tile's
+    // FIR and stores)
+    auto load_tile = [&](int tb) {
+        const int iy0 = (blockIdx.y * TPB + tb) * kFH - pady0;
 #pragma unroll
         for (int l = 0; l < NL; ++l) {
             const int i = tid + 256 * l;
             const int r = i / G4, q = i - r * G4;
             const int iy = iy0 + r;
-            const int64_t row = pbase + (int64_t)iy * tp_w;
-            const int64_t g0 = ((row + ox0 - 4) & ~(int64_t)3) + 4 * q;
-            gx[l] = (int)(g0 - row);
+            const int row = pmis + iy * tp_w;                 // of the aligned base
+            const int g0 = ((row + ox0 - 4) & ~3) + 4 * q;
+            gx[l] = g0 - row;
             const bool ok = i < ROWS * G4 && iy >= 0 && iy < t_h && gx[l] + 3 >= 0 && gx[l] < t_w;
             off[l] = ok ? g0 : -1;
-            v[l] = *reinterpret_cast<const float4*>(t + (ok ? g0 : 0));
+            v[l] = *reinterpret_cast<const float4*>(tpl + (ok ? g0 : 0));
         }
+    };
+    if (blockIdx.y * TPB * kFH < y_h) load_tile(0);
+    for (int tb = 0; tb < TPB; ++tb) {
+        const int oy0 = (blockIdx.y * TPB + tb) * kFH;
+        if (oy0 >= y_h) break;
+        if (tb > 0) __syncthreads();  // the previous tile's FIR reads are done
+        if (!SMC_BLUR_PIPE && tb > 0) load_tile(tb);
         for (int s = 1; s < nsplit; ++s) {
-            const float* sp = t + s * split_stride;
+            const float* sp = tpl + s * split_stride;
 #pragma unroll
             for (int l = 0; l < NL; ++l) {
                 const float4 a = *reinterpret_cast<const float4*>(sp + (off[l] >= 0 ? off[l] : 0));
@@ -416,6 +460,7 @@ __global__ __launch_bounds__(256) void blur_act_v4(const float* t, int nsplit, i
             }
         }
         __syncthreads();
+        if (SMC_BLUR_PIPE && tb + 1 < TPB && oy0 + kFH < y_h) load_tile(tb + 1);
         float out[4][2];
         fir_block<FH, FW>(tile, STRIDE, 4 * ty, 2 * tx, tp, out);
         const int64_t plane = nc * (int64_t)y_h * y_w;
@@ -895,7 +940,8 @@ SMC_API int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_s
                                      int t_h, int t_w, int t_pitch, int y_h, int y_w, const float* f, int fh, int fw,
                                      int padx0, int pady0, float fgain, int flip, const smc_conv_epilogue* epi,
                                      void* stream) {
-    SMC_CHECK(t && y && f && n >= 1 && c >= 1 && nsplit >= 1, "smc_modconv_blur_act_f32: bad args");
+    SMC_CHECK(t && y && (f || (fh == 4 && fw == 4)) && n >= 1 && c >= 1 && nsplit >= 1,
+              "smc_modconv_blur_act_f32: bad args");
     if (fh > kMaxF || fw > kMaxF || fh < 1 || fw < 1) {
         smc::set_error("smc_modconv_blur_act_f32: filter %dx%d > %dx%d", fh, fw, kMaxF, kMaxF);
         return SMC_ERR_UNSUPPORTED;
@@ -913,8 +959,12 @@ SMC_API int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_s
                         epi->noise_nstride % 2 == 0 && padx0 <= 4 && fw - 1 - padx0 <= 4;
         if (v4) {
             grid.y = (unsigned)smc::ceil_div((int)grid.y, SMC_BLUR_TPB);
-            hipLaunchKernelGGL((blur_act_v4<4, 4, SMC_BLUR_TPB, SMC_BLUR_NT != 0>), grid, dim3(256), 0, st, t, nsplit, split_stride, y, c, t_h, t_w, tp_w,
-                               y_h, y_w, f, padx0, pady0, fgain, flip, to_epi(epi));
+            if (SMC_BLUR_STDF && !f && fgain == 4.f)   // the built-in resample filter with the conv0 gain: compile-time taps
+                hipLaunchKernelGGL((blur_act_v4<4, 4, SMC_BLUR_TPB, SMC_BLUR_NT != 0, true>), grid, dim3(256), 0, st, t, nsplit,
+                                   split_stride, y, c, t_h, t_w, tp_w, y_h, y_w, f, padx0, pady0, fgain, flip, to_epi(epi));
+            else
+                hipLaunchKernelGGL((blur_act_v4<4, 4, SMC_BLUR_TPB, SMC_BLUR_NT != 0>), grid, dim3(256), 0, st, t, nsplit,
+                                   split_stride, y, c, t_h, t_w, tp_w, y_h, y_w, f, padx0, pady0, fgain, flip, to_epi(epi));
         } else {
             hipLaunchKernelGGL((blur_act_fast<4, 4>), grid, dim3(256), 0, st, t, nsplit, split_stride, y, c, t_h, t_w,
                                tp_w, y_h, y_w, f, padx0, pady0, fgain, flip, to_epi(epi));

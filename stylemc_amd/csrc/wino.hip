@@ -33,6 +33,17 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// A/B knobs (SMC_AB_DEFINES builds a variant library): the forward's style scale folded into per-image U (kept:
+// r = 512 / 1024 forward 426 -> 407 / 497 -> 489 us, profiles/r05/wino_ab/); the accumulators cleared by each one's
+// first MFMA (zero C operand, the loop peeled) instead of 128 v_mov per item (not kept: the data gradient 396 -> 401 /
+// 473 -> 479 us -- twice the loop code for ~10 % of the VALU stream)
+#ifndef SMC_WINO_FOLD
+#define SMC_WINO_FOLD 1
+#endif
+#ifndef SMC_WINO_ZEROC
+#define SMC_WINO_ZEROC 0
+#endif
+
 constexpr int WBK = 8;    // input channels per K step
 constexpr int WBO = 32;   // output channels per workgroup
 constexpr int WBT = 64;   // tiles per workgroup (4 waves x 16)
@@ -59,6 +70,7 @@ struct WinoParams {
     int nsplit;            // K splits (grid.y): > 1 stores raw partial tiles (EK 3) for smc_modconv_epilogue_f32
     int64_t split_stride;  // floats between the partial planes of two splits
     float* ws;             // the partial planes [nsplit][n][cout][h][w]
+    int64_t u_nstride;     // 0: one U for the batch; else floats between per-image U (s[n, c] folded in)
 };
 
 // Staged row pitch: CHP >= CH 16-B chunks (the pad chunks are sentinel DMA lanes, zero-filled) so that a channel slab
@@ -129,8 +141,8 @@ void wino_kernel(WinoParams p) {
     const int total = p.n * p.gx * p.gy * p.ntn;
     const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * plane * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ursrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.uw, (short)0, p.cin * 16 * p.cout * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ursrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.uw, (short)0, (p.u_nstride ? p.n : 1) * p.cin * 16 * p.cout * 4, 0x00020000);
 
     // work item v -> (image, tile group, output-channel block) through the XCD-aware bijective order of conv_gemm.hip
     // (items v and v + 8 run on one XCD when the grid is a multiple of 8; output-channel blocks fastest, so the
@@ -169,9 +181,9 @@ void wino_kernel(WinoParams p) {
     };
     // step ks of an item into LDS slot `slot`: the U slab [8][4][32][4] and the raw input rows of the block's
     // (2 TR + 2) x (2 TC + 8) patch (16-B chunks from column 2 tx0 - 4, zero-filled by the buffer range check)
-    auto issue = [&](const int (&uv)[UJW], const int (&pv)[PJW], int ks, int slot) {
+    auto issue = [&](const int (&uv)[UJW], const int (&pv)[PJW], int ks, int slot, int nn) {
         float* us = smem + slot * STAGE;
-        const int uso = (kb + ks) * (WBK * 16 * 4) * p.cout;
+        const int uso = (kb + ks) * (WBK * 16 * 4) * p.cout + nn * (int)p.u_nstride * 4;
 #pragma unroll
         for (int j = 0; j < ((PROBE & 1) != 0 && ks > 0 ? 0 : UJW); ++j) {
             const int vo = uv[j];  // (through a local: hipcc drops the kernel's host stub when the array is passed)
@@ -205,7 +217,7 @@ void wino_kernel(WinoParams p) {
     WinoItem it = decode(v);
     int uv[UJW], pv[PJW];
     offsets(it, uv, pv);
-    issue(uv, pv, 0, 0);
+    issue(uv, pv, 0, 0, it.nn);
     const float* srow = has_s ? p.s + (int64_t)it.nn * p.cin + kb * WBK + kq_lane : p.x;
     float sv[2] = {1.f, 1.f}, sn[2] = {1.f, 1.f};
     if (has_s) { sn[0] = srow[0]; sn[1] = srow[4]; }
@@ -266,19 +278,26 @@ void wino_kernel(WinoParams p) {
             vv[4 * i + 3] = (t[i][1] - t[i][3]) * sc;
         }
     };
-    auto mma_group = [&](int g, const f32x4 (&a)[OBW], const float (&vv)[16]) {
+    // ZERO: the first product into each accumulator of an item takes a zero C operand (an inline constant of the
+    // MFMA) instead of accumulators cleared by 128 v_mov per item
+    auto mma_group = [&](int g, const f32x4 (&a)[OBW], const float (&vv)[16], auto zero_c) {
+        constexpr bool ZERO = decltype(zero_c)::value;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int b = 0; b < OBW; ++b)
-                acc[4 * g + j][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[b][j], vv[4 * g + j], acc[4 * g + j][b], 0, 0, 0);
+                acc[4 * g + j][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                    a[b][j], vv[4 * g + j], ZERO ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[4 * g + j][b], 0, 0, 0);
     };
+    using NZ = std::false_type;
 
     for (;;) {
+        if constexpr (!SMC_WINO_ZEROC) {
 #pragma unroll
-        for (int xi = 0; xi < 16; ++xi)
+            for (int xi = 0; xi < 16; ++xi)
 #pragma unroll
-            for (int b = 0; b < OBW; ++b) acc[xi][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int b = 0; b < OBW; ++b) acc[xi][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
         const int vn = v + stride;
         const bool has_next = PERSIST && vn < total;
         WinoItem nx = it;
@@ -292,13 +311,13 @@ void wino_kernel(WinoParams p) {
             asm volatile("" ::: "memory");
             sv[0] = sn[0]; sv[1] = sn[1];
             if (ks + 1 < nsteps) {
-                issue(uv, pv, ks + 1, (gs + 1) & 1);
+                issue(uv, pv, ks + 1, (gs + 1) & 1, it.nn);
                 if (has_s) { sn[0] = srow[(ks + 1) * WBK]; sn[1] = srow[(ks + 1) * WBK + 4]; }
             } else if (has_next) {  // the next item's first step, under this item's last MFMAs and its epilogue
                 nx = decode(vn);
                 int uvn[UJW], pvn[PJW];
                 offsets(nx, uvn, pvn);
-                issue(uvn, pvn, 0, (gs + 1) & 1);
+                issue(uvn, pvn, 0, (gs + 1) & 1, nx.nn);
                 if (has_s) {
                     srow_n = p.s + (int64_t)nx.nn * p.cin + kq_lane;
                     sn[0] = srow_n[0]; sn[1] = srow_n[4];
@@ -311,7 +330,7 @@ void wino_kernel(WinoParams p) {
             load_patch(ps, 0);
             load_a(us, 0, ar[0]);
             __builtin_amdgcn_sched_barrier(0);
-            if (pend) mma_group(3, ar[1], vb);  // the previous step's last group
+            if (pend) mma_group(3, ar[1], vb, NZ{});  // the previous step's last group
             __builtin_amdgcn_sched_barrier(0);
             transform(sv[0], va);
             __builtin_amdgcn_sched_barrier(0);
@@ -320,11 +339,13 @@ void wino_kernel(WinoParams p) {
                 if (gi + 1 < 8) load_a(us, gi + 1, ar[(gi + 1) & 1]);
                 if (gi == 0) load_patch(ps, 1);
                 __builtin_amdgcn_sched_barrier(0);
-                if (gi < 7) {
-                    mma_group(gi & 3, ar[gi & 1], gi < 4 ? va : vb);
+                if (SMC_WINO_ZEROC && gi < 4 && ks == 0) {
+                    mma_group(gi, ar[gi & 1], va, std::true_type{});   // each accumulator's first product
+                } else if (gi < 7) {
+                    mma_group(gi & 3, ar[gi & 1], gi < 4 ? va : vb, NZ{});
                 } else {
                     pend = ks + 1 < nsteps;
-                    if (!pend) mma_group(3, ar[1], vb);
+                    if (!pend) mma_group(3, ar[1], vb, NZ{});
                 }
                 if (gi == 3) {
                     transform(sv[1], vb);
@@ -455,6 +476,22 @@ void wino_kernel(WinoParams p) {
     }
 }
 
+// Per-image U with the style folded in: out[nn][c][...] = uw[c][...] * s[nn][c] (float4 runs of the [cin][4][cout][4]
+// layout).  The forward's x s[n, c] then costs nothing in the kernel's input transform (16 multiplies per patch and
+// channel, ~10 % of its VALU stream, which shares the SIMD issue port with the fp32 MFMA).
+__global__ __launch_bounds__(256) void wino_ufold_kernel(const float4* uw, const float* s, float4* out, int cin,
+                                                         int per4, int64_t total4) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total4; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t nn = e / per4;
+        const int r = (int)(e - nn * per4);
+        const int c = r / (per4 / cin);
+        const float sc = s[nn * cin + c];
+        float4 v = uw[r];
+        v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
+        out[e] = v;
+    }
+}
+
 // U = G g G^T per (k, n): flip = 0: g = w[n][k] (k = cin, n = cout: the forward correlation);
 // flip = 1: g = w[k][n] rotated by 180 degrees (k = cout, n = cin: the data gradient).  Out: [K][4][N][4].
 __global__ __launch_bounds__(256) void wino_weights_kernel(const float* w, int cout, int cin, int flip, float* uw) {
@@ -548,6 +585,17 @@ int wino_nsplit(int n, int cin, int cout, int h, int w) {
     return ns;
 }
 
+// The fold applies where the per-image U is small (the 32 / 64-channel layers: 64 / 256 KB per image).
+constexpr int64_t kWinoFoldMaxCinCout = 128 * 128;
+int64_t wino_fold_bytes(int n, int cin, int cout) {
+    return (int64_t)cin * cout <= kWinoFoldMaxCinCout ? (int64_t)n * cin * 16 * cout * 4 : 0;
+}
+int64_t wino_split_bytes(int n, int cin, int cout, int h, int w) {
+    const int ns = wino_nsplit(n, cin, cout, h, w);
+    return ns > 1 ? (((int64_t)ns * n * cout * h * w * 4 + 255) / 256) * 256 : 0;
+}
+
+
 }  // namespace
 
 SMC_API int smc_conv3x3_wino_supported(int n, int cin, int cout, int h, int w) {
@@ -565,10 +613,10 @@ SMC_API int smc_wino_weights_f32(const float* w, int cout, int cin, int flip, fl
     return smc::check_launch("smc_wino_weights_f32");
 }
 
+// [split-K partial planes (when the grid is too small)][per-image folded U (forward with a style scale)]
 SMC_API int64_t smc_conv3x3_wino_workspace_size(int n, int cin, int cout, int h, int w) {
     if (!smc_conv3x3_wino_supported(n, cin, cout, h, w)) return 0;
-    const int ns = wino_nsplit(n, cin, cout, h, w);
-    return ns > 1 ? (int64_t)ns * n * cout * h * w * 4 : 0;
+    return wino_split_bytes(n, cin, cout, h, w) + wino_fold_bytes(n, cin, cout);
 }
 
 SMC_API int smc_conv3x3_wino_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
@@ -611,8 +659,25 @@ SMC_API int smc_conv3x3_wino_ws_f32(const float* x, int n, int cin, int h, int w
     // split K when the caller passed the workspace smc_conv3x3_wino_workspace_size() asks for (without one: one
     // workgroup per item over the whole K range, as before)
     const int64_t need = smc_conv3x3_wino_workspace_size(n, cin, cout, h, w);
+    const int64_t split_bytes = wino_split_bytes(n, cin, cout, h, w), fold_bytes = wino_fold_bytes(n, cin, cout);
+    const bool ws_ok = need > 0 && workspace && workspace_bytes >= need;
+    if (SMC_WINO_FOLD && s_in && fold_bytes > 0 && ws_ok) {
+        float* uf = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + split_bytes);
+        SMC_CHECK((reinterpret_cast<uintptr_t>(uf) & 15) == 0, "smc_conv3x3_wino_ws_f32: workspace alignment");
+        const int per4 = cin * 4 * cout;   // float4 per image
+        const int64_t total4 = (int64_t)n * per4;
+        hipLaunchKernelGGL(wino_ufold_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(total4, 256), 4096)),
+                           dim3(256), 0, st, reinterpret_cast<const float4*>(uw), s_in, reinterpret_cast<float4*>(uf),
+                           cin, per4, total4);
+        const int rc = smc::check_launch("smc_conv3x3_wino_ws_f32 (style fold)");
+        if (rc != SMC_OK) return rc;
+        p.uw = uf;
+        p.u_nstride = (int64_t)cin * 16 * cout;
+        p.s = nullptr;
+        s_in = nullptr;
+    }
     p.nsplit = 1;
-    if (need > 0 && workspace && workspace_bytes >= need) {
+    if (split_bytes > 0 && ws_ok) {
         SMC_CHECK((reinterpret_cast<uintptr_t>(workspace) & 7) == 0, "smc_conv3x3_wino_ws_f32: workspace alignment");
         p.nsplit = wino_nsplit(n, cin, cout, h, w);
         p.split_stride = (int64_t)n * cout * h * w;

@@ -272,6 +272,10 @@ class LayerSpec:
         self.bias = bias.detach().float().contiguous() if bias is not None else None
         self.up = up
         self.filter = resample_filter.detach().float().contiguous() if resample_filter is not None else None
+        # the synthesis' setup_filter([1,3,3,1]): the FIR forward kernel takes it as compile-time taps (f = NULL)
+        k = torch.tensor([1.0, 3.0, 3.0, 1.0])
+        self.std_filter = self.filter is not None and tuple(self.filter.shape) == (4, 4) and torch.equal(
+            self.filter.detach().cpu(), torch.outer(k, k) / 64.0)
         self.demodulate = demodulate
         self.act = act
         self.alpha = alpha
@@ -337,10 +341,10 @@ def _modconv_fwd(ctx, x, styles, spec, noise, strength, gain, clamp, need_dx, ne
         t = torch.empty(n, P.cout, th, tw, device=x.device, dtype=torch.float32)
         gemm(x, t, phases, nph, cin, P.cout, s=styles, epi=_epilogue(_hip.EPI_STORE),
              alg_flops=conv_flops(n, cin, P.cout, h, w, 9), alg_bytes=4 * x.numel() + 4 * t.numel() + wbytes)
-        f = spec.filter.to(x.device)
-        fh, fw = f.shape
+        f = None if spec.std_filter else spec.filter.to(x.device)
         _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, P.cout, th, tw, 0, r_h, r_w,
-                  _hip.ptr(f), fh, fw, 1, 1, 4.0, 0, ctypes.byref(epi), _hip.stream())
+                  _hip.ptr(f), 4 if f is None else f.shape[0], 4 if f is None else f.shape[1], 1, 1, 4.0, 0,
+                  ctypes.byref(epi), _hip.stream())
     ctx.spec, ctx.gain, ctx.clamp = spec, gain, clamp
     ctx.noise, ctx.nstride, ctx.strength = nz, nstride, strength
     ctx.from_y = from_y

@@ -147,3 +147,35 @@ def test_identical_steps_bit_equal_ffhq1024():
     for a, b in zip(*runs):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b), (a - b).abs().max()
+
+
+def test_x3_vs_exact_fp32_direction_ffhq1024(monkeypatch):
+    """The split-bf16 direct convs (modconv.X3, the default) against the exact-fp32 MFMA on the whole find_direction
+    step: FFHQ-1024, batch 4, two steps from the same start, fresh generators per product form.  The two directions
+    must agree far tighter than either agrees with the CPU oracle (cosine of the updates >= 0.99999, max-norm
+    relative difference <= 2e-3; the oracle tests allow 0.999 / 1e-2) -- the x3 error is fp32-class end to end."""
+    from stylemc_amd import build, modconv, networks
+    from stylemc_amd.clip_loss import CLIPLoss
+    from stylemc_amd.find_direction import DirectionFinder, initial_delta
+    from stylemc_amd.id_loss import IDLoss
+    build.build(verbose=False)
+    text = synthetic.text_direction("a photo of a face of a feminine woman", "a photo of a face of a man")
+    styles = synthetic.synthetic_styles(8, seed=5).to(DEV)
+    cfg = synthetic.generator_config(resolution=1024)
+    init = initial_delta(0, 0.01)
+    out = {}
+    for form in (True, False):
+        monkeypatch.setattr(modconv, "X3", form)
+        G = networks.build_generator(cfg, synthetic.generator_state_dict(cfg, seed=0), device=DEV)
+        f = DirectionFinder(G, styles, [(CLIPLoss(DEV, text_features=text, synthetic_weights=True, seed=4), 1.0)],
+                            IDLoss(device=DEV, weights=None, seed=3), resolution=1024, batch_size=4, n_epochs=2,
+                            seed=2, init_delta=init)
+        for _ in range(2):
+            f.step()
+        out[form] = (f.delta.cpu().double().flatten() - init.double().flatten())
+    a, b = out[True], out[False]
+    cos = torch.nn.functional.cosine_similarity(a, b, dim=0).item()
+    err = ((a - b).abs().max() / b.abs().max()).item()
+    print(f"x3 vs fp32: update cosine {cos:.9f}, max-norm rel diff {err:.3e}")
+    assert cos >= 0.99999, cos
+    assert err <= 2e-3, err

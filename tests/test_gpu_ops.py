@@ -53,14 +53,6 @@ def _gpu():
     torch.backends.cuda.matmul.allow_tf32 = False
 
 
-@pytest.fixture(params=[True, False], ids=["x3", "fp32"])
-def x3(request, monkeypatch):
-    """Both product forms of the direct GEMM: split-bf16 (modconv.X3, the default) and the exact-fp32 MFMA."""
-    from stylemc_amd import modconv
-    monkeypatch.setattr(modconv, "X3", request.param)
-    return request.param
-
-
 ACTS = ["linear", "relu", "lrelu", "tanh", "sigmoid", "elu", "selu", "softplus", "swish"]
 
 
@@ -243,78 +235,109 @@ def test_synthesis_layer_grad_subsets():
     close(dxc, dxa, 1e-6, "dx only")
 
 
+def _both_forms(monkeypatch, run, what):
+    """run() -> [(gpu result, fp64 reference), ...] once with split-bf16 products (modconv.X3) and once with the
+    exact-fp32 MFMA.  Exact fp32: within 2e-5 of the max vs fp64 (no activation, so no kinks).  Split-bf16: within
+    2x the exact-fp32 kernel's own error on the same inputs, in max and in relative norm (the
+    three dropped cross terms of a split product are <= 2^-23 |a b|, one fp32 rounding)."""
+    from stylemc_amd import modconv
+    errs = {}
+    for form in (False, True):
+        monkeypatch.setattr(modconv, "X3", form)
+        out = []
+        for got, ref in run(form):
+            got = got.detach().double().cpu()
+            scale = max(ref.abs().max().item(), 1e-12)
+            out.append(((got - ref).abs().max().item() / scale, ((got - ref).norm() / ref.norm()).item()))
+        errs[form] = out
+    for k, ((f_max, f_norm), (x_max, x_norm)) in enumerate(zip(errs[False], errs[True])):
+        assert f_max <= 2e-5, f"{what}[{k}] exact fp32: max err {f_max:.3e}"
+        assert x_max <= 2 * f_max, f"{what}[{k}] x3 max err {x_max:.3e} > 2 x fp32 {f_max:.3e}"
+        assert x_norm <= 2 * f_norm, f"{what}[{k}] x3 norm err {x_norm:.3e} > 2 x fp32 {f_norm:.3e}"
+
+
 @pytest.mark.parametrize("n,cin,cout,r", [(2, 32, 32, 256), (4, 64, 32, 128), (1, 32, 32, 1024), (2, 64, 64, 128),
                                            (1, 96, 64, 256), (2, 64, 64, 256), (1, 128, 128, 128), (1, 256, 256, 128),
                                            (2, 512, 512, 16), (4, 512, 512, 8), (3, 128, 64, 24)])
-def test_conv_gemm_same3x3_vs_conv2d(n, cin, cout, r, x3):
+def test_conv_gemm_same3x3_vs_conv2d(n, cin, cout, r, monkeypatch):
     """3x3 'same' convs (conv1 forward with per-sample style-scaled weights, and its data gradient with the
-    shared flipped weights) against an fp64 CPU convolution (no activation, so no kinks: tolerance 2e-5 of the
-    max).  Exact-fp32 MFMA: 32 / 64 output channels with W % 256 == 0 run the row-halo kernel (conv_row_kernel,
-    both tile widths), the other shapes the tap-major LDS-DMA kernel; split-bf16 (x3): every shape the LDS-DMA
-    tiles with split products (per-sample split weights in the forward, split-K at 8 and 16 px)."""
+    shared flipped weights) against an fp64 CPU convolution.  Exact-fp32 MFMA: 32 / 64 output channels with
+    W % 256 == 0 run the row-halo kernel (conv_row_kernel, both tile widths), the other shapes the tap-major LDS-DMA
+    kernel; split-bf16: every shape the LDS-DMA tiles with split products (per-sample split weights in the forward,
+    split-K at 8 and 16 px)."""
     import torch.nn.functional as F
     from stylemc_amd import _hip, modconv
     gen = torch.Generator().manual_seed(11)
     W = torch.randn(cout, cin, 3, 3, generator=gen)
-    P = modconv.PackedConv(W.to(DEV), 1)
     x = torch.randn(n, cin, r, r, generator=gen)
     s = torch.randn(n, cin, generator=gen) * 0.5 + 1
-    ph, nph, _, _ = P.fwd_phases(r, r)
-    y = torch.empty(n, cout, r, r, device=DEV)
-    modconv.gemm(x.to(DEV), y, ph, nph, cin, cout, s=s.to(DEV), epi=modconv._epilogue(_hip.EPI_STORE))
-    ref = F.conv2d((x * s[:, :, None, None]).double(), W.double(), padding=1)
-    close(y, ref, 2e-5, "fwd")
     g = torch.randn(n, cout, r, r, generator=gen)
-    phb, nphb = P.bwd_phases(r, r)
-    dx = torch.empty(n, cin, r, r, device=DEV)
-    modconv.gemm(g.to(DEV), dx, phb, nphb, cout, cin, epi=modconv._epilogue(_hip.EPI_STORE))
+    ref = F.conv2d((x * s[:, :, None, None]).double(), W.double(), padding=1)
     refb = F.conv_transpose2d(g.double(), W.double(), padding=1)
-    close(dx, refb, 2e-5, "data grad")
-    assert (P.x3_fwd is not None) == x3
+
+    def run(form):
+        P = modconv.PackedConv(W.to(DEV), 1)
+        ph, nph, _, _ = P.fwd_phases(r, r)
+        y = torch.empty(n, cout, r, r, device=DEV)
+        modconv.gemm(x.to(DEV), y, ph, nph, cin, cout, s=s.to(DEV), epi=modconv._epilogue(_hip.EPI_STORE))
+        phb, nphb = P.bwd_phases(r, r)
+        dx = torch.empty(n, cin, r, r, device=DEV)
+        modconv.gemm(g.to(DEV), dx, phb, nphb, cout, cin, epi=modconv._epilogue(_hip.EPI_STORE))
+        assert (P.x3_fwd is not None) == form
+        return [(y, ref), (dx, refb)]
+
+    _both_forms(monkeypatch, run, "3x3 fwd / data grad")
 
 
 @pytest.mark.parametrize("n,cin,cout,h", [(2, 64, 32, 64), (1, 32, 32, 128), (2, 512, 512, 4), (3, 256, 128, 16),
                                            (1, 128, 64, 64)])
-def test_conv_gemm_stride2_gather_vs_conv2d(n, cin, cout, h, x3):
+def test_conv_gemm_stride2_gather_vs_conv2d(n, cin, cout, h, monkeypatch):
     """The up = 2 layers' data gradient through the transposed conv: the stride-2 3x3 gather over dT (2h + 1 rows,
-    a padded pitch) against an fp64 conv2d(stride 2) of the same dT -- both product forms (tolerance 2e-5 of the
-    max)."""
+    a padded pitch) against an fp64 conv2d(stride 2) of the same dT, both product forms (_both_forms)."""
     import torch.nn.functional as F
     from stylemc_amd import _hip, modconv
     gen = torch.Generator().manual_seed(17)
     W = torch.randn(cout, cin, 3, 3, generator=gen)
-    P = modconv.PackedConv(W.to(DEV), 2)
     th = 2 * h + 1
     g = torch.randn(n, cout, th, th, generator=gen)
-    phb, nphb = P.bwd_phases(h, h)
-    dx = torch.empty(n, cin, h, h, device=DEV)
-    modconv.gemm(g.to(DEV), dx, phb, nphb, cout, cin, epi=modconv._epilogue(_hip.EPI_STORE))
     ref = F.conv2d(g.double(), W.transpose(0, 1).double(), stride=2)
-    assert ref.shape == dx.shape, (ref.shape, dx.shape)
-    close(dx, ref, 2e-5, "stride-2 gather")
-    assert (P.x3_bwd is not None) == x3
+
+    def run(form):
+        P = modconv.PackedConv(W.to(DEV), 2)
+        phb, nphb = P.bwd_phases(h, h)
+        dx = torch.empty(n, cin, h, h, device=DEV)
+        modconv.gemm(g.to(DEV), dx, phb, nphb, cout, cin, epi=modconv._epilogue(_hip.EPI_STORE))
+        assert ref.shape == dx.shape, (ref.shape, dx.shape)
+        assert (P.x3_bwd is not None) == form
+        return [(dx, ref)]
+
+    _both_forms(monkeypatch, run, "stride-2 gather")
 
 
 @pytest.mark.parametrize("n,cin,cout,h", [(2, 64, 32, 64), (1, 128, 64, 128), (2, 512, 512, 4), (3, 256, 128, 16),
                                            (1, 512, 256, 32), (2, 32, 32, 33), (4, 512, 512, 8)])
-def test_conv_gemm_transposed_vs_conv_transpose2d(n, cin, cout, h, x3):
+def test_conv_gemm_transposed_vs_conv_transpose2d(n, cin, cout, h, monkeypatch):
     """The up = 2 layers' stride-2 transposed 3x3 conv (conv2d_resample.py:125-138 before the blur) as the
     phase-fused LDS-DMA kernel: per-sample style-scaled weights with tiles restarted per image ((h+1)^2 not a
     tile multiple), a prescaled input at the low resolutions, split-K over channel chunks; vs fp64
-    conv_transpose2d (tolerance 2e-5 of the max)."""
+    conv_transpose2d, both product forms (_both_forms)."""
     import torch.nn.functional as F
     from stylemc_amd import _hip, modconv
     gen = torch.Generator().manual_seed(13)
     W = torch.randn(cout, cin, 3, 3, generator=gen)
-    P = modconv.PackedConv(W.to(DEV), 2)
     x = torch.randn(n, cin, h, h, generator=gen)
     s = torch.randn(n, cin, generator=gen) * 0.5 + 1
-    ph, nph, th, tw = P.fwd_phases(h, h)
-    t = torch.empty(n, cout, th, tw, device=DEV)
-    modconv.gemm(x.to(DEV), t, ph, nph, cin, cout, s=s.to(DEV), epi=modconv._epilogue(_hip.EPI_STORE))
     ref = F.conv_transpose2d((x * s[:, :, None, None]).double(), W.transpose(0, 1).double(), stride=2)
-    close(t, ref, 2e-5, "transposed conv")
-    assert all((w is not None) == x3 for w in P.x3_phases)
+
+    def run(form):
+        P = modconv.PackedConv(W.to(DEV), 2)
+        ph, nph, th, tw = P.fwd_phases(h, h)
+        t = torch.empty(n, cout, th, tw, device=DEV)
+        modconv.gemm(x.to(DEV), t, ph, nph, cin, cout, s=s.to(DEV), epi=modconv._epilogue(_hip.EPI_STORE))
+        assert all((w is not None) == form for w in P.x3_phases)
+        return [(t, ref)]
+
+    _both_forms(monkeypatch, run, "transposed conv")
 
 
 def _misaligned(t):
@@ -346,12 +369,12 @@ def test_blur_act_load_paths(n, c, h):
     bias = (torch.randn(c, generator=gen) * 0.1).to(DEV)
     st = _hip.stream()
 
-    def fwd(tbuf, pitch):
+    def fwd(tbuf, pitch, builtin=False):
         y = torch.empty(n, c, r, r, device=DEV)
         u = torch.empty_like(y)
         epi = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 1.0, u)
         _hip.call("smc_modconv_blur_act_f32", tbuf.data_ptr(), 1, 0, y.data_ptr(), n, c, th, th, pitch, r, r,
-                  f.data_ptr(), 4, 4, 1, 1, 4.0, 0, ctypes.byref(epi), st)
+                  None if builtin else f.data_ptr(), 4, 4, 1, 1, 4.0, 0, ctypes.byref(epi), st)
         return y, u
 
     y0, u0 = fwd(T, 0)
@@ -359,8 +382,12 @@ def test_blur_act_load_paths(n, c, h):
     Tp[..., :th] = T
     y1, u1 = fwd(Tp, th + 7)
     y2, u2 = fwd(_misaligned(T), 0)
+    y3, u3 = fwd(T, 0, builtin=True)               # f = NULL: compile-time [1,3,3,1] taps (16-B kernel)
+    y4, u4 = fwd(_misaligned(T), 0, builtin=True)  # ... and the scalar-load kernel's built-in taps
     torch.cuda.synchronize()
-    for a, b, what in ((y1, y0, "y pitched"), (u1, u0, "u pitched"), (y2, y0, "y scalar"), (u2, u0, "u scalar")):
+    for a, b, what in ((y1, y0, "y pitched"), (u1, u0, "u pitched"), (y2, y0, "y scalar"), (u2, u0, "u scalar"),
+                       (y3, y0, "y built-in taps"), (u3, u0, "u built-in taps"), (y4, y0, "y scalar built-in"),
+                       (u4, u0, "u scalar built-in")):
         assert torch.equal(a, b), what
     ref = F.conv2d(F.pad(T.double().cpu(), (1, 1, 1, 1)).view(n * c, 1, th + 2, th + 2),
                    (4.0 * f.double().cpu().flip(0, 1))[None, None]).view(n, c, r, r)

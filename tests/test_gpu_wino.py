@@ -53,8 +53,12 @@ SHAPES = [  # n, cin, cout, h, w  (TC 16 / 32 / 64 block shapes, non-square, 512
 ]
 
 
+@pytest.mark.parametrize("ws", [False, True], ids=["in_kernel_scale", "workspace"])
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
-def test_wino_forward_vs_fp64(shape):
+def test_wino_forward_vs_fp64(shape, ws):
+    """Style-scaled forward.  Without a workspace the kernel scales each transformed patch by s[n, c]; with the
+    workspace smc_conv3x3_wino_workspace_size asks for, the 32..128-channel shapes take per-image U with s folded in
+    (wino_ufold_kernel) and the 512-channel 32 x 32 one splits K."""
     H = _lib()
     n, cin, cout, h, w = shape
     g = torch.Generator().manual_seed(sum(shape))
@@ -66,8 +70,14 @@ def test_wino_forward_vs_fp64(shape):
     uw = torch.empty(16 * cin * cout, device=DEV)
     H.call("smc_wino_weights_f32", Wd.data_ptr(), cout, cin, 0, uw.data_ptr(), H.stream())
     y = torch.empty(n, cout, h, w, device=DEV)
-    H.call("smc_conv3x3_wino_f32", xd.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(), sd.data_ptr(),
-           None, H.stream())
+    if ws:
+        nb = H.load().smc_conv3x3_wino_workspace_size(n, cin, cout, h, w)
+        wsb = torch.full((max(nb // 4, 1),), float("nan"), device=DEV)
+        H.call("smc_conv3x3_wino_ws_f32", xd.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(),
+               sd.data_ptr(), None, wsb.data_ptr(), nb, H.stream())
+    else:
+        H.call("smc_conv3x3_wino_f32", xd.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(), sd.data_ptr(),
+               None, H.stream())
     torch.cuda.synchronize()
     if n * h * w > 1 << 20:  # the 1024-px case: check two images' worth of rows (fp64 conv on CPU is slow)
         y, x, s = y[:, :, :64], x[:, :, :66], s
@@ -211,7 +221,7 @@ def test_wino_split_plan():
     assert lib.smc_conv3x3_wino_workspace_size(4, 512, 512, 32, 32) == 2 * 4 * 512 * 32 * 32 * 4
     assert lib.smc_conv3x3_wino_workspace_size(2, 512, 512, 32, 32) == 4 * 2 * 512 * 32 * 32 * 4
     assert lib.smc_conv3x3_wino_workspace_size(4, 512, 512, 64, 64) == 0     # 1024 items: one pass
-    assert lib.smc_conv3x3_wino_workspace_size(2, 32, 32, 32, 32) == 0       # 4 K steps: nothing to split
+    assert lib.smc_conv3x3_wino_workspace_size(2, 32, 32, 32, 32) == 2 * 32 * 16 * 32 * 4  # no split; folded U
     assert lib.smc_conv3x3_wino_workspace_size(1, 512, 512, 16, 16) == 0     # no kernel
 
 

@@ -15,6 +15,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from stylemc_amd import _hip, modconv  # noqa: E402
 
 
+# f = NULL: the built-in [1,3,3,1] taps, as modconv passes for the synthesis' resample filter (--file-taps: f given)
+BUILTIN = "--file-taps" not in sys.argv
+
+
 def timeit(fn, iters=30):
     for _ in range(3):
         fn()
@@ -49,8 +53,8 @@ def main():
         st = _hip.stream()
 
         def blur():
-            _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, c, th, th, 0, r, r, f.data_ptr(),
-                      4, 4, 1, 1, 4.0, 0, ctypes.byref(epi), st)
+            _hip.call("smc_modconv_blur_act_f32", t.data_ptr(), 1, 0, y.data_ptr(), n, c, th, th, 0, r, r,
+                      None if BUILTIN else f.data_ptr(), 4, 4, 1, 1, 4.0, 0, ctypes.byref(epi), st)
         us = timeit(blur)
         total += us
         byt = 4 * (t.numel() + y.numel())

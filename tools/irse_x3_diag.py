@@ -1,5 +1,9 @@
 """Diagnostic: IR-SE50 input gradient with split-bf16 vs exact-fp32 direct GEMMs, against fp64 (max and norm error,
-cosine, how many PReLU pre-activations change sign between the two forms).
+cosine), and the conditioning of that gradient itself: the fp64 reference re-run on inputs perturbed by one fp32
+rounding (x * (1 + 2^-24 r), r ~ N(0, 1)) -- how far the EXACT gradient moves when the input moves by the error any
+fp32 implementation makes.  If that move is as large as the x3 / fp32 errors, the errors are the input gradient's
+own discontinuity (a PReLU / SE-ReLU pre-activation within rounding of its kink takes the other branch), not lost
+product bits.
 
     python tools/irse_x3_diag.py
 """
@@ -25,9 +29,16 @@ def main():
         xr = x.double().requires_grad_(True)
         (dxr,) = torch.autograd.grad(ref(xr), xr, cot.double())
         scale = dxr.abs().max().item()
+        for k in range(3):   # the exact gradient at inputs one fp32 rounding away
+            r = torch.randn(x.shape, generator=gen, dtype=torch.float64)
+            xp = (x.double() * (1 + 2.0 ** -24 * r)).requires_grad_(True)
+            (dxp,) = torch.autograd.grad(ref(xp), xp, cot.double())
+            print(f"n={n} fp64 at x(1 + 2^-24 r) #{k}: max move {(dxp - dxr).abs().max().item() / scale:.3e}  "
+                  f"norm move {((dxp - dxr).norm() / dxr.norm()).item():.3e}  elements beyond 1e-4 of max: "
+                  f"{int(((dxp - dxr).abs() > 1e-4 * scale).sum())}", flush=True)
         res = {}
         for x3 in (False, True):
-            modconv.X3 = x3
+            irse_hip.X3 = x3
             hip = irse_hip.build_irse50(seed=3, device="cuda")
             xg = x.cuda().requires_grad_(True)
             yg = hip(xg)
