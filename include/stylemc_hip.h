@@ -216,7 +216,7 @@ int smc_modconv_blur_act_f32(const float* t, int nsplit, int64_t split_stride, f
  * dt = adjoint FIR of du (pad (pady0, padx0) = (fh-1-p, fw-1-p) of the forward pad p, flip, gain fgain;
  * upfirdn2d.py:245-264 rule), and if dd != NULL: dd[n,o] += sum_hw dz*u.  g/u: [n,c,u_h,u_w],
  * dt: [n,c,t_h,t_pitch] (t_pitch = 0: t_w; columns >= t_w are not written).  4x4 filters only
- * (SMC_ERR_UNSUPPORTED otherwise). */
+ * (SMC_ERR_UNSUPPORTED otherwise); f = NULL: the built-in [1,3,3,1] taps (as smc_modconv_blur_act_f32). */
 int smc_modconv_blur_act_bwd_f32(const float* g, const float* u, float* dt, float* dd, int n, int c, int u_h, int u_w,
                                  int t_h, int t_w, int t_pitch, const float* f, int fh, int fw, int padx0, int pady0,
                                  float fgain, int flip, const smc_conv_epilogue* epi, void* workspace,

@@ -692,6 +692,11 @@ __global__ __launch_bounds__(256) void x3_weights_kernel(const float* wk, const 
 #ifndef SMC_X3_WO1
 #define SMC_X3_WO1 1
 #endif
+// ... with 16-channel K steps (half the LDS per stage: 3 workgroups per CU instead of 2; A/B knob).  Measured
+// (profiles/r05/ab5/, two interleaved rounds on one box): 468.96 / 467.66 against 467.77 / 466.56 images/s.
+#ifndef SMC_X3_WO1_K16
+#define SMC_X3_WO1_K16 1
+#endif
 // Timing probes only (0 in the library; tools/ builds a variant with SMC_AB_DEFINES): 1 drops the input DMAs after
 // the first K step, 2 the weight DMAs after the first, 4 the register split (the fp32 bits reused as the three terms)
 #ifndef SMC_X3_PROBE
@@ -2157,7 +2162,9 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             // 32-channel K steps for the narrow tiles too (A/B knob SMC_X3_K32_SMALL: half the barriers per FLOP)
             const bool k32s = SMC_X3_K32_SMALL && cin % 32 == 0;
             g_last_x3 = 1;
-            if (SMC_X3_WO1 && cfg == 0 && k32 && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 4, 1, 32>), grid, dim3(NT), 0, st, p);
+            if (SMC_X3_WO1 && SMC_X3_WO1_K16 && cfg == 0 && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 4, 1, 16>), grid, dim3(NT), 0, st, p);
+            else if (SMC_X3_WO1 && SMC_X3_WO1_K16 && cfg == 5 && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 2, 1, 16>), grid, dim3(NT), 0, st, p);
+            else if (SMC_X3_WO1 && cfg == 0 && k32 && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 4, 1, 32>), grid, dim3(NT), 0, st, p);
             else if (SMC_X3_WO1 && cfg == 5 && k32s && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 2, 1, 32>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0 && k32 && tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32, SMC_X3_NST, 1>), grid, dim3(NT), 0, st, p);
             else if (cfg == 0 && k32) hipLaunchKernelGGL((conv_gemm_x3_kernel<2, 2, 2, 2, 32>), grid, dim3(NT), 0, st, p);

@@ -73,7 +73,10 @@ def adj_weight(W, ky, kx, in_scale=None, out_scale=None):
 # input gradient of these seeded weights is ill-conditioned (PReLU kinks: the fp32 CPU path itself is 6.4e-3 of the max
 # away from fp64 at 4 / 8 faces), and the split products move which kinks flip -- x3 1e-6 / 3e-3 / 6e-3 against fp32
 # 1e-4 / 8e-5 / 9e-7 at 4 / 1 / 8 faces, cosine >= 0.9999994 either way (profiles/r04/irse_x3_diag.txt) -- for a
-# 0.1 ms / step kernel-time gain.  The reference-pinned tolerances stay those of the exact-fp32 products.
+# 0.1 ms / step kernel-time gain (r05: +0.7 % images/s, profiles/r05/ab5/).  Round 5 showed the flips are the gradient's
+# own: the fp64 gradient at an input one fp32 rounding away moves by up to 4.9e-3 of the max
+# (profiles/r05/x3_accuracy/irse_x3_conditioning.txt).  The reference-pinned tolerances stay those of the exact-fp32
+# products.
 X3 = False
 
 

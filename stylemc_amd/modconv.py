@@ -391,8 +391,8 @@ def _modconv_bwd(ctx, saved, gy, need_dx, need_ds, g=None):
                       u.shape[2], u.shape[3], ctypes.byref(epi), _hip.ptr(ws), _nbytes(ws), _hip.stream())
         else:
             # fused: epilogue backward + adjoint of FIR(pad 1, gain 4) (pad fw-1-1 = 2, correlation) + dd
-            f = spec.filter.to(x.device)
-            fh, fw = f.shape
+            f = None if spec.std_filter else spec.filter.to(x.device)
+            fh, fw = (4, 4) if f is None else f.shape
             # dT rows padded to a multiple of 4 floats (aligned 16-B row starts for the FIR's stores and the gather
             # GEMM's loads); the stride-2 gather reads columns <= 2w only, so the pad columns are never read.
             th, tw = 2 * h + 1, 2 * w + 1

@@ -408,16 +408,20 @@ def test_blur_act_load_paths(n, c, h):
     dt1, dd1 = bwd(_misaligned(g), _misaligned(u0))
     _, dd0b = bwd(g, u0)
 
-    def bwd_from_y(gb, yb):   # grad_from_y: the saved forward output instead of u, no dd
+    def bwd_from_y(gb, yb, builtin=False):   # grad_from_y: the saved forward output instead of u, no dd
         dt = torch.full((n, c, th, th), float("nan"), device=DEV)
         epi = modconv._epilogue(_hip.EPI_MODACT, d, noise, 0, strength, bias, "lrelu", 0.2, 2 ** 0.5, 1.0)
         epi.grad_from_y = 1
         _hip.call("smc_modconv_blur_act_bwd_f32", gb.data_ptr(), yb.data_ptr(), dt.data_ptr(), None, n, c,
-                  r, r, th, th, 0, f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epi), None, 0, st)
+                  r, r, th, th, 0, None if builtin else f.data_ptr(), 4, 4, 2, 2, 4.0, 1, ctypes.byref(epi), None, 0,
+                  st)
         return dt
 
     dt2 = bwd_from_y(g, y0)
     dt3 = bwd_from_y(_misaligned(g), _misaligned(y0))
+    dt4 = bwd_from_y(g, y0, builtin=True)              # built-in [1,3,3,1] taps (16-B kernel)
+    dt5 = bwd_from_y(_misaligned(g), _misaligned(y0), builtin=True)
+    assert torch.equal(dt4, dt2) and torch.equal(dt5, dt2), "dT built-in taps vs the filter tensor"
     torch.cuda.synchronize()
     assert torch.isfinite(dt0).all()
     assert torch.equal(dt0, dt1), "dT scalar vs 16-B loads"
