@@ -142,8 +142,9 @@ typedef struct {
 } smc_conv_epilogue;
 
 /* bytes of workspace smc_conv_gemm_f32 needs for these sizes (0 = none). */
-/* 1 if the last smc_conv_gemm_f32 call of this thread launched the split-bf16 kernels (the phases carried wk_x3 and
- * the LDS-DMA tiles took the shape), 0 if it ran exact-fp32 products (timing / roofline attribution). */
+/* nonzero if the last smc_conv_gemm_f32 call of this thread launched the split-bf16 kernels (the phases carried wk_x3
+ * and the LDS-DMA tiles took the shape; 2: the 256-channel wide tile), 0 if it ran exact-fp32 products (timing /
+ * roofline attribution, tests). */
 int smc_conv_gemm_last_x3(void);
 int64_t smc_conv_gemm_workspace_size(int n, int cin, int cout, int y_h, int y_w, const smc_conv_phase* phases,
                                      int nphases);

@@ -703,10 +703,22 @@ __global__ __launch_bounds__(256) void x3_weights_kernel(const float* wk, const 
 #define SMC_X3_PROBE 0
 #endif
 
-template <int WO, int WM, int TO, int TM, int BKT, int NST = SMC_X3_NST, int TAG = 0>
+// Wide tiles (AS: 256 output channels x 128 positions, each wave 256 x 32): the K step's input DMAs and its B split
+// are amortised over twice the MFMAs of the 128-channel tile (per wave and step: 8 input + 6 weight DMAs, 44 split
+// VALU for 48 MFMAs, against 8 + 3 and 44 for 24), the issue budget the 128-channel tile overruns.  The A fragments
+// are read one output block ahead of its MFMAs instead of all at once (128 accumulator registers leave no room for
+// 8 x 3 fragments).  Only where the 256-channel grid needs no split-K, for shared weights (A/B knob SMC_X3_WIDE).
+// Measured it gains less than the issue count suggests (-5 % on the r = 256 data gradient, +2 % on the style-scaled
+// r = 128 forward): the 128-channel tile is not bound by its DMA + split issue alone.
+#ifndef SMC_X3_WIDE
+#define SMC_X3_WIDE 1
+#endif
+
+template <int WO, int WM, int TO, int TM, int BKT, int NST = SMC_X3_NST, int TAG = 0, bool AS = false>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
     static_assert(WO * WM == 4, "4 waves");
     static_assert(BKT % 16 == 0, "16-channel chunks");
+    static_assert(!AS || (BKT == 16 && TM == 1 && NST == 2), "streamed A fragments: one 16-channel chunk per step");
     constexpr int BO = WO * TO * 32;
     constexpr int BM = WM * TM * 32;
     constexpr int NKC = BKT / 16;                // 16-channel chunks per K step (one bf16 MFMA K each)
@@ -852,6 +864,31 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
         const short* Wp = reinterpret_cast<const short*>(st);
         const float* Xs = reinterpret_cast<const float*>(st + WB);
         const float* xcol = Xs + wm * TM * 32 + l32;
+        if constexpr (AS) {
+            float xw[8];
+            bf16x8 ar[2][3];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xw[e] = xcol[(8 * kh + e) * BM];
+            auto read_a = [&](int i, int b) {
+#pragma unroll
+                for (int s = 0; s < 3; ++s)
+                    ar[b][s] = *reinterpret_cast<const bf16x8*>(Wp + (((s * 2 + kh) * BO) + wo * TO * 32 + i * 32 + l32) * 8);
+            };
+            read_a(0, 0);
+            if (issued < ks_end) {  // the next step's DMAs under this step's first reads
+                issue(issued, (issued - ks_begin) % NST);
+                ++issued;
+            }
+            bf16x8 bw[3];
+            x3_split8(xw, bw);
+#pragma unroll
+            for (int i = 0; i < TO; ++i) {
+                if (i + 1 < TO) read_a(i + 1, (i + 1) & 1);
+                acc[i][0] = x3_mma(ar[i & 1], bw, acc[i][0]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            continue;
+        }
         // Chunk pipeline: chunk kc + 1's fragment reads and input split are issued in the same region as chunk kc's
         // MFMAs (no scheduling fence between them), so the LDS latency and the split VALU fill the MFMA issue gaps.
         float xv[2][TM][8];
@@ -913,6 +950,22 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_x3_kernel(GemmParams p) {
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragment reads of this slot done before the next barrier
+    }
+    if constexpr (AS) {
+        // two 128-channel halves (the 8-block body is not unrolled by the compiler: the accumulators would go to
+        // scratch for a dynamically indexed epilogue)
+        static_assert(WO == 1 && TO % 2 == 0, "halves");
+        f32x16 lo[TO / 2][TM], hi[TO / 2][TM];
+#pragma unroll
+        for (int i = 0; i < TO / 2; ++i) {
+            lo[i][0] = acc[i][0];
+            hi[i][0] = acc[TO / 2 + i][0];
+        }
+        gemm_epilogue<WO, WM, TO / 2, TM>(p, ph, lo, m0, o0, M, hw_out, split, wo, wm, kh, l32,
+                                          reinterpret_cast<float*>(smem));
+        gemm_epilogue<WO, WM, TO / 2, TM>(p, ph, hi, m0, o0 + (TO / 2) * 32, M, hw_out, split, wo, wm, kh, l32,
+                                          reinterpret_cast<float*>(smem));
+        return;
     }
     gemm_epilogue<WO, WM, TO, TM>(p, ph, acc, m0, o0, M, hw_out, split, wo, wm, kh, l32,
                                   reinterpret_cast<float*>(smem));
@@ -1936,7 +1989,10 @@ namespace {
 // Split-K target of the IR-SE50 executor's GEMMs (TAG 1), in workgroups per CU: its 7..28-px stages are
 // latency-bound chains of small GEMMs where more, shorter splits pay (tools/prof_irse.py, IR-SE50 pair
 // fwd(8) + bwd(4): 2 -> 4.34 ms, 4 -> 4.16; 1 -> 4.99).  The synthesis keeps 2.
-constexpr int kSplitPerCuAux = 4;
+#ifndef SMC_AUX_SPLIT_PER_CU
+#define SMC_AUX_SPLIT_PER_CU 4
+#endif
+constexpr int kSplitPerCuAux = SMC_AUX_SPLIT_PER_CU;
 
 int64_t workspace_size_impl(int n, int cin, int cout, int y_h, int y_w, const smc_conv_phase* phases, int nphases,
                             int split_per_cu) {
@@ -2000,6 +2056,15 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
     if (!fused_t && !convt_lds && small_tile_ok(n, cin, cout, in_h, in_w, phases, nphases, s_in != nullptr, c)) {
         cfg = 3;
         c = Cfg{64, 64};
+    }
+    // split-bf16 wide tiles (conv_gemm_x3_kernel AS): 256 output channels where that grid fills the chip unsplit, for
+    // shared weights only.  Measured (profiles/r05/x3_wide/, tools/bench_gemm.py): the r = 256 stride-2 data gradient
+    // 226.3 -> 215.6 us; the style-scaled r = 128 transposed conv0 (per-sample weights) 259.9 -> 265.2, so not there.
+    if (SMC_X3_WIDE && x3 && !tag && !s_in && cfg == 0 && !fused_t && !convt_lds && cout % 256 == 0 &&
+        plan_split(n, cin, cout, phases, nphases, Cfg{256, 128}) == 1 &&
+        lds_shape_ok(n, cin, cout, in_h, in_w, phases, nphases, Cfg{256, 128}, nullptr)) {
+        cfg = 6;
+        c = Cfg{256, 128};
     }
     const bool t_per_sample = convt_lds && s_in && ((int64_t)(in_h + 1) * (in_w + 1)) % tl.bm != 0;
     const int nsplit = convt_lds ? plan_split_convt_lds(n, cin, cout, in_h, in_w, tl, t_per_sample)
@@ -2161,8 +2226,9 @@ int conv_gemm_impl(const float* x, int n, int cin, int in_h, int in_w, float* y,
             const bool k32 = cfg == 0 && cin % 32 == 0;
             // 32-channel K steps for the narrow tiles too (A/B knob SMC_X3_K32_SMALL: half the barriers per FLOP)
             const bool k32s = SMC_X3_K32_SMALL && cin % 32 == 0;
-            g_last_x3 = 1;
-            if (SMC_X3_WO1 && SMC_X3_WO1_K16 && cfg == 0 && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 4, 1, 16>), grid, dim3(NT), 0, st, p);
+            g_last_x3 = cfg == 6 ? 2 : 1;
+            if (cfg == 6) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 8, 1, 16, 2, 0, true>), grid, dim3(NT), 0, st, p);
+            else if (SMC_X3_WO1 && SMC_X3_WO1_K16 && cfg == 0 && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 4, 1, 16>), grid, dim3(NT), 0, st, p);
             else if (SMC_X3_WO1 && SMC_X3_WO1_K16 && cfg == 5 && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 2, 1, 16>), grid, dim3(NT), 0, st, p);
             else if (SMC_X3_WO1 && cfg == 0 && k32 && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 4, 1, 32>), grid, dim3(NT), 0, st, p);
             else if (SMC_X3_WO1 && cfg == 5 && k32s && !tag) hipLaunchKernelGGL((conv_gemm_x3_kernel<1, 4, 2, 1, 32>), grid, dim3(NT), 0, st, p);

@@ -665,10 +665,14 @@ bool lin_v2_ok(int N, int K, int lda, int ldb) {
     return K % L2K == 0 && N % L2N == 0 && lda % 4 == 0 && ldb % 4 == 0;
 }
 
+// A/B knob: plan the split for 1 / SMC_LIN_CU_DIV of the CUs (the loss networks run beside each other)
+#ifndef SMC_LIN_CU_DIV
+#define SMC_LIN_CU_DIV 1
+#endif
 int lin_nsplit2(int M, int N, int K) {
     const int64_t tiles = smc::ceil_div(smc::plan_rows(M), L2M) * (N / L2N);
     const int nks = K / L2K;
-    const int64_t cus = smc::device_cu_count();
+    const int64_t cus = std::max<int64_t>(1, smc::device_cu_count() / SMC_LIN_CU_DIV);
     int best = 1;
     int64_t best_cost = -1;
     for (int s = 1; s <= 16 && s <= nks; ++s) {

@@ -340,6 +340,45 @@ def test_conv_gemm_transposed_vs_conv_transpose2d(n, cin, cout, h, monkeypatch):
     _both_forms(monkeypatch, run, "transposed conv")
 
 
+@pytest.mark.parametrize("kind", ["transposed", "stride2"])
+def test_conv_gemm_x3_wide_tile(kind, monkeypatch):
+    """The split-bf16 wide tile (256 output channels x 128 positions, conv_gemm_x3_kernel AS: A fragments streamed per
+    output block, the epilogue in two halves) where its grid fills the chip unsplit -- one image planned as 16
+    (_hip.plan_batch), the r = 128 conv0 forward / r = 256 data-gradient shapes of the 4-image step: vs fp64, both
+    product forms (_both_forms), and the library reports the wide launch (smc_conv_gemm_last_x3 == 2)."""
+    import torch.nn.functional as F
+    from stylemc_amd import _hip, modconv
+    gen = torch.Generator().manual_seed(23)
+    lib = _hip.load()
+    if kind == "transposed":
+        cin, cout, h = 512, 256, 32
+        W = torch.randn(cout, cin, 3, 3, generator=gen)
+        x = torch.randn(1, cin, h, h, generator=gen)
+        s = torch.randn(1, cin, generator=gen) * 0.5 + 1
+        ref = F.conv_transpose2d((x * s[:, :, None, None]).double(), W.transpose(0, 1).double(), stride=2)
+    else:
+        cin, cout, h = 256, 128, 64   # the forward's channels; the data gradient has cin = 256 outputs
+        W = torch.randn(cout, cin, 3, 3, generator=gen)
+        g = torch.randn(1, cout, 2 * h + 1, 2 * h + 1, generator=gen)
+        ref = F.conv2d(g.double(), W.transpose(0, 1).double(), stride=2)
+
+    def run(form):
+        P = modconv.PackedConv(W.to(DEV), 2)
+        with _hip.plan_batch(16, 1):
+            if kind == "transposed":
+                ph, nph, th, tw = P.fwd_phases(h, h)
+                out = torch.empty(1, cout, th, tw, device=DEV)
+                modconv.gemm(x.to(DEV), out, ph, nph, cin, cout, s=s.to(DEV), epi=modconv._epilogue(_hip.EPI_STORE))
+            else:
+                phb, nphb = P.bwd_phases(h, h)
+                out = torch.empty(1, cin, h, h, device=DEV)
+                modconv.gemm(g.to(DEV), out, phb, nphb, cout, cin, epi=modconv._epilogue(_hip.EPI_STORE))
+            assert lib.smc_conv_gemm_last_x3() == (2 if form else 0)
+        return [(out, ref)]
+
+    _both_forms(monkeypatch, run, f"wide tile {kind}")
+
+
 def _misaligned(t):
     """A copy of `t` whose data pointer is 4 B past a 16-B boundary (forces the scalar-load kernels)."""
     buf = torch.empty(t.numel() + 1, device=t.device, dtype=t.dtype)
