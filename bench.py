@@ -93,6 +93,8 @@ def parse():
                    help="CLIP ViT projections: split-bf16 (x3) or exact-fp32 MFMA GEMMs (vit_hip.X3)")
     p.add_argument("--irse-products", default=None, choices=["x3", "fp32"],
                    help="IR-SE50 executor GEMMs: split-bf16 or exact-fp32 (irse_hip.X3; default: the library's)")
+    p.add_argument("--prefetch-id", default=None, choices=["on", "off"],
+                   help="the original image's IR-SE50 features on the prefetch stream (default: DirectionFinder's)")
     p.add_argument("--schedule", default="prefetch", choices=["pair", "prefetch"],
                    help="stream schedule: pair = original synthesis beside the edited one; prefetch = the next "
                         "iteration's original synthesis on a third stream (DESIGN.md section 6b)")
@@ -349,7 +351,8 @@ def main():
     finder = DirectionFinder(G, styles, clip, IDLoss("a", device=dev, weights=None, impl=args.id_impl), resolution=args.resolution,
                              batch_size=args.batch, global_batch=args.batch * world.world_size, seed=0, world=world,
                              init_delta=initial_delta(0, 0.01), n_epochs=1000,
-                             batch_losses=not args.no_batch_losses, prefetch_orig=args.schedule != "pair")
+                             batch_losses=not args.no_batch_losses, prefetch_orig=args.schedule != "pair",
+                             **({} if args.prefetch_id is None else {"prefetch_id": args.prefetch_id == "on"}))
     for _ in range(args.warmup):
         finder.step()
     torch.cuda.synchronize()

@@ -345,7 +345,8 @@ int smc_layernorm_bwd_f32(const float* dy, int64_t lddy, const float* x, int64_t
 
 /* Multi-head softmax attention over qkv [batch*tokens][3*heads*64] (q | k | v, nn.MultiheadAttention
  * in_proj order) -> out [batch*tokens][heads*64]; p_save [batch][heads][tokens][tokens] may be NULL.
- * head_dim must be 64.  The backward writes dqkv [batch*tokens][3*heads*64]. */
+ * head_dim must be 64.  The backward writes dqkv [batch*tokens][3*heads*64] and needs qkv and dout 16-byte
+ * aligned. */
 int smc_attention_fwd_f32(const float* qkv, float* out, float* p_save, int batch, int tokens, int heads,
                           int head_dim, float scale, void* stream);
 int smc_attention_bwd_f32(const float* dout, const float* qkv, const float* p_save, float* dqkv, int batch,

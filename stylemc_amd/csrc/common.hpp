@@ -66,6 +66,13 @@ __device__ __forceinline__ float epi_y(float u, float d, float nz, float bias, i
     return clamp_fwd(act_fwd(act, z, alpha) * gain, clamp);
 }
 
+// The compile-time lrelu + gain + clamp body of the synthesis epilogues (0 <= alpha <= 1, clamp >= 0): lrelu(z) =
+// max(z, alpha z) and the clamp as one v_med3_f32 (= min(max(., -clamp), clamp) for every non-NaN value), bit-identical
+// to epi_y for finite values.
+__device__ __forceinline__ float lrelu_gain_clamp(float z, float alpha, float gain, float clamp) {
+    return __builtin_amdgcn_fmed3f(fmaxf(z, z * alpha) * gain, -clamp, clamp);
+}
+
 // Epilogue fields beyond the modconv ones (IR-SE50 modes, per-channel scale, strided residual).
 struct EpiExt {
     const float* scale_c;

@@ -172,7 +172,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const PhaseDe
                                                        (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
                         if constexpr (KIND == 1) {  // max / min forms: bit-identical to epi_y for finite values
                             const float z = __fmaf_rn(v, dd, nz) + lds[BO + ol];
-                            q = fmaxf(fminf(fmaxf(z, z * p.alpha) * p.gain, p.clamp), -p.clamp);
+                            q = smc::lrelu_gain_clamp(z, p.alpha, p.gain, p.clamp);
                         } else if constexpr (KIND == 2) {
                             q = (__fmaf_rn(v, dd, nz) + lds[BO + ol]) * p.gain;
                         } else {

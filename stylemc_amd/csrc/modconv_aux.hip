@@ -496,8 +496,8 @@ __global__ __launch_bounds__(256, STDF ? SMC_BLUR_WGS : 1) void blur_act_v4(cons
             float2 q;
             if (lrelu_clamp) {
                 const float zx = __fmaf_rn(u2.x, dv, nz[i].x) + bv, zy = __fmaf_rn(u2.y, dv, nz[i].y) + bv;
-                q.x = fmaxf(fminf(fmaxf(zx, zx * e.alpha) * e.gain, e.clamp), -e.clamp);
-                q.y = fmaxf(fminf(fmaxf(zy, zy * e.alpha) * e.gain, e.clamp), -e.clamp);
+                q.x = smc::lrelu_gain_clamp(zx, e.alpha, e.gain, e.clamp);
+                q.y = smc::lrelu_gain_clamp(zy, e.alpha, e.gain, e.clamp);
             } else {
                 q = make_float2(smc::epi_y(u2.x, dv, nz[i].x, bv, e.act, e.alpha, e.gain, e.clamp),
                                 smc::epi_y(u2.y, dv, nz[i].y, bv, e.act, e.alpha, e.gain, e.clamp));

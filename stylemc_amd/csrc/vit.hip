@@ -255,6 +255,10 @@ int lin_validate(const float* a, int lda, const float* b, int ldb, const float* 
 // one L2.
 constexpr int L2M = 32, L2N = 64, L2K = 64;
 
+// The hand-off's partial-tile loads as sc1 (L1-bypassing) agent loads (diagnostic knob)
+#ifndef SMC_LIN_SC1LOAD
+#define SMC_LIN_SC1LOAD 0
+#endif
 #ifndef SMC_LIN_NST
 #define SMC_LIN_NST 2
 #endif
@@ -444,7 +448,8 @@ __global__ __launch_bounds__(256 * KW, 2) void lin_gemm2_kernel(LinParams p, int
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int m = min(m0 + wm * 16 + 4 * g + rr, p.M - 1);
-                const float t = part[(int64_t)m * p.N + n0 + wn * 32 + blk * 16 + i];
+                const float* src = part + (int64_t)m * p.N + n0 + wn * 32 + blk * 16 + i;
+                const float t = SMC_LIN_SC1LOAD ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *src;
                 v[blk][rr] = k == 0 ? t : v[blk][rr] + t;
             }
     }
@@ -646,7 +651,8 @@ __global__ __launch_bounds__(256, 2) void lin_gemm2_x3_kernel(LinParams p, const
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int m = min(m0 + wm * 16 + 4 * g + rr, p.M - 1);
-                const float t = part[(int64_t)m * p.N + n0 + wn * 32 + blk * 16 + i];
+                const float* src = part + (int64_t)m * p.N + n0 + wn * 32 + blk * 16 + i;
+                const float t = SMC_LIN_SC1LOAD ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *src;
                 v[blk][rr] = k == 0 ? t : v[blk][rr] + t;
             }
     }
@@ -665,9 +671,15 @@ bool lin_v2_ok(int N, int K, int lda, int ldb) {
     return K % L2K == 0 && N % L2N == 0 && lda % 4 == 0 && ldb % 4 == 0;
 }
 
-// A/B knob: plan the split for 1 / SMC_LIN_CU_DIV of the CUs (the loss networks run beside each other)
+// In-launch split-K hand-off in the executor's GEMMs (0: the separate reduction kernel; diagnostic knob)
+#ifndef SMC_LIN_INLAUNCH
+#define SMC_LIN_INLAUNCH 1
+#endif
+// Split-K planned for 1 / SMC_LIN_CU_DIV of the CUs: in the step CLIP runs beside IR-SE50 (and the prefetched
+// synthesis), and fewer, longer splits leave CUs to the other chain.  Measured (profiles/r05/loss_split/, interleaved):
+// 1 -> 2: 469.1 -> 471.0 images/s over three rounds (459.3 / 463.9 -> 466.8 / 467.0 in the first A/B); 4: 471.1.
 #ifndef SMC_LIN_CU_DIV
-#define SMC_LIN_CU_DIV 1
+#define SMC_LIN_CU_DIV 2
 #endif
 int lin_nsplit2(int M, int N, int K) {
     const int64_t tiles = smc::ceil_div(smc::plan_rows(M), L2M) * (N / L2N);
@@ -873,6 +885,57 @@ __device__ __forceinline__ void stage_rows64(float* dst, const float* src, int64
     }
 }
 
+// Several row blocks of 64 floats (16-B aligned rows, ld % 4 == 0) into LDS rows of pitch HP in ONE batch of 16-B
+// loads: up to KMAX float4 per thread are in flight before the first LDS store (the K, V, Q, dO blocks of an attention
+// backward workgroup: one global round trip instead of one per 2048-element chunk of each block; 28.8 -> 27.8 us per
+// launch, profiles/r05/attn_stage/).
+struct StageSeg {
+    float* dst;
+    const float* src;
+    int64_t ld;
+    int rows, valid;
+    float mul;
+};
+
+template <int NSEG, int KMAX>
+__device__ __forceinline__ void stage_segs(const StageSeg (&s)[NSEG]) {
+    int start[NSEG + 1];
+    start[0] = 0;
+#pragma unroll
+    for (int i = 0; i < NSEG; ++i) start[i + 1] = start[i] + s[i].rows * (HD / 4);
+    const int total = start[NSEG];
+    for (int g0 = 0; g0 < total; g0 += 256 * KMAX) {
+        float4 v[KMAX];
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int g = g0 + (int)threadIdx.x + 256 * k;
+            int si = 0;
+#pragma unroll
+            for (int i = 1; i < NSEG; ++i) si = g >= start[i] ? i : si;
+            const int loc = min(g, total - 1) - start[si];
+            const int row = min(loc >> 4, s[si].valid - 1);
+            v[k] = *reinterpret_cast<const float4*>(s[si].src + (int64_t)row * s[si].ld + 4 * (loc & 15));
+        }
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int g = g0 + (int)threadIdx.x + 256 * k;
+            if (g >= total) continue;
+            int si = 0;
+#pragma unroll
+            for (int i = 1; i < NSEG; ++i) si = g >= start[i] ? i : si;
+            const int loc = g - start[si];
+            const int row = loc >> 4, c = 4 * (loc & 15);
+            const bool ok = row < s[si].valid;
+            const float m = s[si].mul;
+            float* d = s[si].dst + row * HP + c;
+            d[0] = ok ? v[k].x * m : 0.f;
+            d[1] = ok ? v[k].y * m : 0.f;
+            d[2] = ok ? v[k].z * m : 0.f;
+            d[3] = ok ? v[k].w * m : 0.f;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* qkv, float* out, float* psave, int L, int H,
                                                        float scale, int causal) {
     extern __shared__ float sm[];
@@ -885,6 +948,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* qkv, float* 
     const int D = H * HD, ld = 3 * D;
     const float* base = qkv + (int64_t)b * L * ld + h * HD;
     const int nq = min(AQB, L - q0);
+    // (row staging: the one-batch 16-B staging of the backward measured slower here, 17.4 -> 20.7 us per launch,
+    // profiles/r05/attn_stage/)
     stage_rows64(Ks, base + D, ld, L, L, 1.f);
     stage_rows64(Vs, base + 2 * D, ld, L, L, 1.f);
     stage_rows64(Qs, base + (int64_t)q0 * ld, ld, AQB, nq, scale);
@@ -942,12 +1007,24 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float* dout, const 
     const int D = H * HD, ld = 3 * D;
     const int nq = min(QB, L - q0);
     const float* base = qkv + (int64_t)b * L * ld + h * HD;
-    stage_rows64(Ks, base + D, ld, L, L, 1.f);
-    stage_rows64(Vs, base + 2 * D, ld, L, L, 1.f);
-    stage_rows64(Qs, base + (int64_t)q0 * ld, ld, QB, nq, scale);
-    stage_rows64(dOs, dout + ((int64_t)b * L + q0) * D + h * HD, D, QB, nq, 1.f);
     const float* pbase = psave + (((int64_t)b * H + h) * L + q0) * L;
-    for (int i0 = tid; i0 < QB * L; i0 += 256 * 8) {  // P block: loads first, as in stage_rows64
+    // P block (contiguous, not 16-B aligned): its first 8 loads per thread are issued before the K / V / Q / dO batch
+    float pv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pv[k] = pbase[min(tid + 256 * k, nq * L - 1)];
+    {
+        const StageSeg segs[4] = {{Ks, base + D, ld, L, L, 1.f},
+                                  {Vs, base + 2 * D, ld, L, L, 1.f},
+                                  {Qs, base + (int64_t)q0 * ld, ld, QB, nq, scale},
+                                  {dOs, dout + ((int64_t)b * L + q0) * D + h * HD, D, QB, nq, 1.f}};
+        stage_segs<4, 10>(segs);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int idx = tid + 256 * k;
+        if (idx < QB * L) Ps[idx] = idx < nq * L ? pv[k] : 0.f;
+    }
+    for (int i0 = tid + 256 * 8; i0 < QB * L; i0 += 256 * 8) {  // the rest of P (QB * L > 2048: long sequences)
         float v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = pbase[min(i0 + 256 * k, nq * L - 1)];
@@ -1034,6 +1111,8 @@ int attn_bwd_launch(const float* dout, const float* qkv, const float* psave, flo
     const int QB = attn_bwd_qb(L);
     const int nqb = (int)smc::ceil_div(L, QB);
     const size_t lds = attn_bwd_lds(L, QB);
+    SMC_CHECK((reinterpret_cast<uintptr_t>(qkv) & 15) == 0 && (reinterpret_cast<uintptr_t>(dout) & 15) == 0,
+              "smc_attention_bwd_f32: qkv and dout must be 16-byte aligned");
     int rc = attn_check_lds(lds, reinterpret_cast<const void*>(attn_bwd_kernel));
     if (rc != SMC_OK) return rc;
     if (nqb > 1 && hipMemsetAsync(dqkv, 0, sizeof(float) * (size_t)B * L * 3 * H * HD, st) != hipSuccess) {
@@ -1519,7 +1598,7 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
     int64_t cursor = 0;
     auto lin = [&](const float* a, int lda, const float* bw, int ldb, float* c, int ldc, int MM, int N, int K,
                    const smc_linear_epilogue& e, const short* bx3, const float* bt) {
-        int* ctr = ws.counters + cursor;
+        int* ctr = SMC_LIN_INLAUNCH ? ws.counters + cursor : nullptr;
         cursor += ws.counter_slice;
         if (cursor > ws.counter_ints) {
             smc::set_error("smc_vit: split-K counter slices exhausted");
@@ -1609,7 +1688,7 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
     int64_t cursor = 0;
     auto lin = [&](const float* a, int lda, const float* bw, int ldb, float* c, int ldc, int MM, int N, int K,
                    const smc_linear_epilogue& e, const short* bx3, const float* bt) {
-        int* ctr = ws.counters + cursor;
+        int* ctr = SMC_LIN_INLAUNCH ? ws.counters + cursor : nullptr;
         cursor += ws.counter_slice;
         if (cursor > ws.counter_ints) {
             smc::set_error("smc_vit: split-K counter slices exhausted");

@@ -439,7 +439,7 @@ void wino_kernel(WinoParams p) {
                                 for (int j = 0; j < 2; ++j) {
                                     if constexpr (KIND == 1) {
                                         const float z = __fmaf_rn(out[i][j], dsc, nz[i][j]) + bo;
-                                        q[j] = fmaxf(fminf(fmaxf(z, z * p.alpha) * p.gain, p.clamp), -p.clamp);
+                                        q[j] = smc::lrelu_gain_clamp(z, p.alpha, p.gain, p.clamp);
                                     } else if constexpr (KIND == 2) {
                                         q[j] = (__fmaf_rn(out[i][j], dsc, nz[i][j]) + bo) * p.gain;
                                     } else {

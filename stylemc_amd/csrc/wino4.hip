@@ -371,7 +371,7 @@ void wino4_kernel(Wino4Params p) {
                 for (int j = 0; j < 4; ++j) {
                     if constexpr (EK == 1) {
                         const float z = __fmaf_rn(out[j], dsc, nz[j]) + bo;
-                        q[j] = fmaxf(fminf(fmaxf(z, z * p.alpha) * p.gain, p.clamp), -p.clamp);
+                        q[j] = smc::lrelu_gain_clamp(z, p.alpha, p.gain, p.clamp);
                     } else if constexpr (EK == 2) {
                         q[j] = (__fmaf_rn(out[j], dsc, nz[j]) + bo) * p.gain;
                     } else {

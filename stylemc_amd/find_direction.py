@@ -316,6 +316,15 @@ class DirectionFinder:
             # the second stream beside CLIP; autograd runs each backward on its forward's stream and joins
             # them where the gradients meet (d img)
             side.wait_stream(main)
+            # every tensor the side stream reads but another stream allocated is recorded on the side stream: freed
+            # on the host while the side stream's kernels still read it (y_feats is freed as soon as the backward has
+            # used it, and its backward runs on the side stream), its block would otherwise go to the next
+            # allocation of its own stream -- the prefetch stream writing the next iteration's image into the
+            # features the ID-loss backward is about to read (run-to-run differences ~1e-5 in delta, tools/det_check.py)
+            img.record_stream(side)
+            for t in (y_feats, orig):
+                if t is not None:
+                    t.record_stream(side)
             with torch.cuda.stream(side):
                 id_terms = (self.id_loss.per_sample_with(img, y_feats) if y_feats is not None
                             else self.id_loss.per_sample_pair(img, orig))
@@ -423,12 +432,17 @@ class DirectionFinder:
         if getattr(self, "_pre", None) is None:
             self._pre = self.stream_factory(self.device)
         self._pre.wait_event(self._fwd_done)
+        if getattr(self, "diag_id_after_bwd", False):
+            self._diag_id_after = torch.cuda.Event()
+            self._diag_id_after.record(torch.cuda.current_stream())
         with torch.cuda.stream(self._pre), torch.no_grad(), self._plan(b - a):
             out = self._prefetch_body(self.styles_array[a:b])
         self._pref = ((a, b),) + out
 
     def _prefetch_body(self, styles):
         orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
+        if self.prefetch_id and getattr(self, "_diag_id_after", None) is not None:
+            torch.cuda.current_stream().wait_event(self._diag_id_after)   # diagnostic (tools/det_check.py)
         feats = self.id_loss.target_feats(orig) if self.prefetch_id else None
         return orig, feats, None
 

@@ -1,8 +1,12 @@
 #!/bin/bash
 # r05: second round of the loss-network split A/B (r05_ab7): base, lin2 / lin4 (ViT GEMMs planned for 1/2, 1/4 of the
-# CUs).  (IR-SE50 planned for 1 workgroup per CU, aux1, flipped a PReLU kink of test_irse50_vs_torch_fp64[1]: dropped.)
+# CUs), on the tree with the one-batch attention staging (its tests + tower times first).  (IR-SE50 planned for 1 workgroup per CU, aux1, flipped a PReLU kink of test_irse50_vs_torch_fp64[1]: dropped.)
 OUT=gpurun_out/${1:-r05_ab8}; ROUNDS=${2:-2}
 mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_vit.py tests/test_gpu_clip_text.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_base.log 2>&1
+rc=$?; echo "base tests rc=$rc: $(tail -1 $OUT/pytest_base.log)"; [ $rc -eq 0 ] || exit 1
+timeout -k 10 200 python tools/bench_vit.py 4 > $OUT/vit4_base.txt 2>&1 && timeout -k 10 200 python tools/bench_vit.py 8 > $OUT/vit8_base.txt 2>&1 || exit 1
+grep hip $OUT/vit4_base.txt $OUT/vit8_base.txt
 SMC_HIP_LIB=_lib_ab/lin4/libstylemc_hip.so timeout -k 10 400 python -u -m pytest tests/test_gpu_irse.py tests/test_gpu_vit.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_lin4.log 2>&1
 rc=$?; echo "lin4 tests rc=$rc: $(tail -1 $OUT/pytest_lin4.log)"; [ $rc -eq 0 ] || exit 1
 run() {  # tag lib extra-args
