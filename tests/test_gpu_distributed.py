@@ -11,7 +11,7 @@ image's gradient row comes back separately and the global batch's rows are summe
 all_gather.  That makes every piece of a shard's step bit-equal to the full batch's (tests/test_gpu_batch_invariance.py)
 and the 8-rank gloo runs bit-exact (tests/test_distributed_cpu.py).  This pipelined schedule itself, however, is not
 run-to-run reproducible on the GPU (round 5, tools/det_check.py: about one run in eight differs from the others, up to
-~2e-3 of the max in delta after three steps, within one process too -- root cause open),
+5e-4 (absolute) in delta after three steps, within one process too -- root cause open),
 so the two-rank run is compared with the single-rank run and with the lockstep replay at tolerance: batch picks
 exact, delta / saved direction / loss terms within 1e-2 of their max and cosine >= 0.9999.
 """
