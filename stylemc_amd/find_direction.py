@@ -307,7 +307,13 @@ class DirectionFinder:
             img = self._synth_edited(styles, d)
             with torch.no_grad():
                 orig = self.synth_fn(self.G, self.until_k, styles, self.temp_shapes, self.noise_mode)
-        if side is not None:
+        if side is not None and getattr(self, "diag_losses_on_main", False):   # diagnostic (tools/det_check.py)
+            self._fwd_done = torch.cuda.Event()
+            self._fwd_done.record(main)
+            id_terms = (self.id_loss.per_sample_with(img, y_feats) if y_feats is not None
+                        else self.id_loss.per_sample_pair(img, orig))
+            side = None
+        elif side is not None:
             # the next iteration's original-image synthesis (prefetch stream) may start from here: it then
             # overlaps the latency-bound loss networks and this iteration's backward
             self._fwd_done = torch.cuda.Event()
@@ -320,7 +326,8 @@ class DirectionFinder:
             # on the host while the side stream's kernels still read it (y_feats is freed as soon as the backward has
             # used it, and its backward runs on the side stream), its block would otherwise go to the next
             # allocation of its own stream -- the prefetch stream writing the next iteration's image into the
-            # features the ID-loss backward is about to read (run-to-run differences ~1e-5 in delta, tools/det_check.py)
+            # features the ID-loss backward is about to read (a hazard found while chasing the pipelined step's
+            # run-to-run differences; not their cause)
             img.record_stream(side)
             for t in (y_feats, orig):
                 if t is not None:

@@ -22,7 +22,7 @@ def main():
     world = sdist.World(0, 1, 0, None, 0)
     gb, n_items, steps = W.CASES[0]
     modes = {"pipelined": {}, "no_prefetch": {"prefetch_orig": False}, "single_stream": {"overlap": False},
-             "pipelined_no_id_prefetch": {"prefetch_id": False}, "pipelined_id_after_bwd": {}}
+             "pipelined_no_id_prefetch": {"prefetch_id": False}, "pipelined_id_after_bwd": {}, "pipelined_losses_on_main": {}}
     names = sys.argv[1].split(",") if len(sys.argv) > 1 else ["pipelined", "no_prefetch", "single_stream"]
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     for name in names:
@@ -33,6 +33,7 @@ def main():
             f = DirectionFinder(G, styles, clip, idl, resolution=W.RES, batch_size=gb, global_batch=gb, n_epochs=4,
                                 seed=1, world=world, init_delta=initial_delta(0, 0.01), temp_shapes=shapes, **kw)
             f.diag_id_after_bwd = name == "pipelined_id_after_bwd"
+            f.diag_losses_on_main = name == "pipelined_losses_on_main"
             rows = []
             for _ in range(steps):
                 last = f.step()
