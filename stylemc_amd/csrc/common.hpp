@@ -20,6 +20,8 @@ int64_t conv_gemm_aux_workspace_size(int n, int cin, int cout, int y_h, int y_w,
                                      int nphases);
 int check_launch(const char* what);
 int device_cu_count();
+// Zero `bytes` (a multiple of 4) at p with a kernel on `st` (in place of hipMemsetAsync; errors.hip).
+int zero_async(void* p, size_t bytes, hipStream_t st, const char* what);
 // Planning batch (smc_set_plan_batch): every launch decision that depends on the batch -- split-K factors, tile
 // configurations, channel splits, all of which change a result's fp32 summation order -- is made for
 // plan_batch(n) images (plan_rows(m) rows of a token-major GEMM) instead of the call's own n.  Default: n itself.

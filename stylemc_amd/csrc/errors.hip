@@ -1,4 +1,5 @@
 // Error state and device queries for the C ABI.
+#include <algorithm>
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
@@ -26,6 +27,24 @@ int check_launch(const char* what) {
         return SMC_ERR_LAUNCH;
     }
     return SMC_OK;
+}
+
+__global__ __launch_bounds__(256) void zero_kernel(uint4* p, int64_t n16, uint32_t* tail, int64_t ntail) {
+    const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, step = (int64_t)gridDim.x * 256;
+    for (int64_t i = i0; i < n16; i += step) p[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int64_t i = i0; i < ntail; i += step) tail[i] = 0u;
+}
+
+int zero_async(void* p, size_t bytes, hipStream_t st, const char* what) {
+    if (bytes == 0) return SMC_OK;
+    const int64_t n16 = ((reinterpret_cast<uintptr_t>(p) & 15) == 0) ? (int64_t)(bytes / 16) : 0;
+    uint32_t* tail = reinterpret_cast<uint32_t*>(static_cast<char*>(p) + n16 * 16);
+    const int64_t ntail = (int64_t)(bytes - n16 * 16) / 4;  // (an unaligned buffer: word stores only)
+    int64_t blocks = std::max<int64_t>(ceil_div(std::max<int64_t>(n16, ntail), 256), 1);
+    blocks = std::min<int64_t>(blocks, (int64_t)device_cu_count() * 8);
+    hipLaunchKernelGGL(zero_kernel, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<uint4*>(p), n16, tail,
+                       ntail);
+    return check_launch(what);
 }
 
 int device_cu_count() {

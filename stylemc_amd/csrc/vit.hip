@@ -21,6 +21,23 @@
 
 #include "common.hpp"
 
+// Zero a buffer on the stream: a kernel (smc::zero_async), or hipMemsetAsync in the SMC_HIP_MEMSET=1 A/B build.
+#ifndef SMC_HIP_MEMSET
+#define SMC_HIP_MEMSET 0
+#endif
+#define SMC_TRY_MEMSET(ptr, bytes, st, what)                                                       \
+    do {                                                                                           \
+        if (SMC_HIP_MEMSET) {                                                                      \
+            if (hipMemsetAsync((ptr), 0, (bytes), (st)) != hipSuccess) {                           \
+                smc::set_error("%s failed", what);                                                 \
+                return SMC_ERR_LAUNCH;                                                             \
+            }                                                                                      \
+        } else {                                                                                   \
+            const int rz_ = smc::zero_async((ptr), (bytes), (st), what);                            \
+            if (rz_ != SMC_OK) return rz_;                                                         \
+        }                                                                                          \
+    } while (0)
+
 namespace {
 
 constexpr int LBM = 32, LBN = 128, LBK = 32, LNT = 256;
@@ -1081,7 +1098,10 @@ size_t attn_fwd_lds(int L) { return sizeof(float) * (size_t)(2 * L * HP + AQB * 
 size_t attn_bwd_lds(int L, int QB) { return sizeof(float) * (size_t)(2 * L * HP + 2 * QB * HP + 2 * QB * L); }
 // L <= 64: two query blocks per head (two adds onto zero commute, so the atomics stay deterministic)
 // and the LDS image stays under 64 KiB; longer sequences: 16-row blocks.
-int attn_bwd_qb(int L) { return L <= AQB_BWD_SINGLE ? (L + 1) / 2 : AQB; }
+#ifndef SMC_ATTN_BWD_ONEBLOCK
+#define SMC_ATTN_BWD_ONEBLOCK 0
+#endif
+int attn_bwd_qb(int L) { return L <= AQB_BWD_SINGLE ? (SMC_ATTN_BWD_ONEBLOCK ? L : (L + 1) / 2) : AQB; }
 
 int attn_check_lds(size_t bytes, const void* fn) {
     if (bytes > 160 * 1024) {
@@ -1115,10 +1135,7 @@ int attn_bwd_launch(const float* dout, const float* qkv, const float* psave, flo
               "smc_attention_bwd_f32: qkv and dout must be 16-byte aligned");
     int rc = attn_check_lds(lds, reinterpret_cast<const void*>(attn_bwd_kernel));
     if (rc != SMC_OK) return rc;
-    if (nqb > 1 && hipMemsetAsync(dqkv, 0, sizeof(float) * (size_t)B * L * 3 * H * HD, st) != hipSuccess) {
-        smc::set_error("smc_attention_bwd_f32: memset failed");
-        return SMC_ERR_LAUNCH;
-    }
+    if (nqb > 1) SMC_TRY_MEMSET(dqkv, sizeof(float) * (size_t)B * L * 3 * H * HD, st, "smc_attention_bwd_f32: memset");
     hipLaunchKernelGGL(attn_bwd_kernel, dim3(nqb, H, B), dim3(256), lds, st, dout, qkv, psave, dqkv, L, H, scale, QB,
                        nqb > 1 ? 1 : 0);
     return smc::check_launch("smc_attention_bwd_f32");
@@ -1365,6 +1382,13 @@ LayerS saved_layer(const VitDims& d, int B, const VitS& s, int l) {
     return t;
 }
 
+#ifndef SMC_VIT_TRACE
+#define SMC_VIT_TRACE 0
+#endif
+__global__ __launch_bounds__(256) void trace_copy_kernel(const float* src, float* dst, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
 // ---------------------------------------------------------------------------------------- workspace
 struct VitWs {
     float *h, *o, *big, *qkv, *P, *xa, *xb, *tok, *patches, *dx, *dh, *mu, *rs, *split;
@@ -1372,6 +1396,7 @@ struct VitWs {
     int* counters;           // split-K tile counters: one slice per GEMM of a pass, zeroed per pass
     int64_t counter_slice;   // ints per GEMM call
     int64_t counter_ints;
+    float* trace;            // SMC_VIT_TRACE builds: intermediates of the backward (tools/det_stage.py)
 };
 
 int64_t max_tiles(const VitDims& d, int B) {
@@ -1425,6 +1450,10 @@ int64_t ws_layout(const VitDims& d, int B, float* base, VitWs* w) {
     t.counter_slice = max_tiles(d, B);
     t.counter_ints = t.counter_slice * gemms_per_pass(d);
     t.counters = reinterpret_cast<int*>(seg(t.counter_ints));
+#if SMC_VIT_TRACE
+    // A/B debug builds only (tools/det_stage.py): snapshots of the backward's intermediates, in execution order
+    t.trace = seg(2 * M * D + (int64_t)d.NL * 12 * M * D + M * D + Mt * D + Mt * d.P);
+#endif
     if (w) *w = t;
     return off;
 }
@@ -1606,10 +1635,7 @@ SMC_API int smc_vit_forward_f32(const smc_vit_config* cfg, const float* packed, 
         }
         return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr, bx3, bt);
     };
-    if (hipMemsetAsync(ws.counters, 0, sizeof(int) * (size_t)ws.counter_ints, st) != hipSuccess) {
-        smc::set_error("smc_vit: counter memset failed");
-        return SMC_ERR_LAUNCH;
-    }
+    SMC_TRY_MEMSET(ws.counters, sizeof(int) * (size_t)ws.counter_ints, st, "smc_vit: counter memset");
 
     // patch embedding + class token + positional embedding, ln_pre
     SMC_TRY(smc_patch_im2col_f32(image, ws.patches, B, d.C, d.G, d.p, 0, stream));
@@ -1696,19 +1722,22 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
         }
         return lin_launch(a, lda, bw, ldb, c, ldc, MM, N, K, &e, ws.split, ws.split_bytes, st, ctr, bx3, bt);
     };
-    if (hipMemsetAsync(ws.counters, 0, sizeof(int) * (size_t)ws.counter_ints, st) != hipSuccess) {
-        smc::set_error("smc_vit: counter memset failed");
-        return SMC_ERR_LAUNCH;
-    }
+    int64_t toff = 0;
+    auto snap = [&](const float* src, int64_t n) {
+        if (SMC_VIT_TRACE) {
+            hipLaunchKernelGGL(trace_copy_kernel, dim3(256), dim3(256), 0, st, src, ws.trace + toff, n);
+            toff += n;
+        }
+    };
+    SMC_TRY_MEMSET(ws.counters, sizeof(int) * (size_t)ws.counter_ints, st, "smc_vit: counter memset");
 
     // head: d(ln_post out) = dout @ proj^T, then ln_post backward into the CLS rows of a zeroed dx
     SMC_TRY(lin(dout, d.E, w.proj_t, D, ws.h, D, B, D, d.E, epi_none(), w.proj_t3, w.proj));
-    if (hipMemsetAsync(ws.dx, 0, sizeof(float) * (size_t)M * D, st) != hipSuccess) {
-        smc::set_error("smc_vit_backward_f32: memset failed");
-        return SMC_ERR_LAUNCH;
-    }
+    SMC_TRY_MEMSET(ws.dx, sizeof(float) * (size_t)M * D, st, "smc_vit_backward_f32: memset");
     SMC_TRY(ln_bwd_launch(ws.h, D, sv.x_out, (int64_t)d.L * D, sv.mupost, sv.rspost, w.lnpost_w, nullptr, 0, ws.dx,
                           (int64_t)d.L * D, B, D, st));
+    snap(ws.h, (int64_t)M * D);  // (the head's B rows; M * D keeps the snapshot sizes uniform)
+    snap(ws.dx, (int64_t)M * D);
 
     const float scale = 1.f / sqrtf((float)HD);
     float* dx = ws.dx;  // gradient w.r.t. the current layer's output stream (updated in place)
@@ -1720,18 +1749,28 @@ SMC_API int smc_vit_backward_f32(const smc_vit_config* cfg, const float* packed,
         e.dact_pre = ls.G;
         e.ld_dact = 4 * D;
         SMC_TRY(lin(dx, D, lw.pr_w, 4 * D, ws.big, 4 * D, M, 4 * D, D, e, lw.pr_w3, lw.pr_wt));   // dG = (dx @ W_proj) * gelu'(G)
+        snap(ws.big, (int64_t)M * 4 * D);
         SMC_TRY(lin(ws.big, 4 * D, lw.fc_w, D, ws.dh, D, M, D, 4 * D, epi_none(), lw.fc_w3, lw.fc_wt));  // dh2 = dG @ W_fc
+        snap(ws.dh, (int64_t)M * D);
         SMC_TRY(ln_bwd_launch(ws.dh, D, ls.x_mid, D, ls.mu2, ls.rs2, lw.ln2_w, dx, D, dx, D, M, D, st));
+        snap(dx, (int64_t)M * D);
         // attention block
         SMC_TRY(lin(dx, D, lw.out_w, D, ws.o, D, M, D, D, epi_none(), lw.out_w3, lw.out_wt));       // dO = dx_mid @ W_out
+        snap(ws.o, (int64_t)M * D);
         SMC_TRY(attn_bwd_launch(ws.o, ls.qkv, ls.P, ws.qkv, B, d.L, d.H, scale, st));
+        snap(ws.qkv, (int64_t)M * 3 * D);
         SMC_TRY(lin(ws.qkv, 3 * D, lw.qkv_w, D, ws.dh, D, M, D, 3 * D, epi_none(), lw.qkv_w3, lw.qkv_wt));  // dh1 = dqkv @ W_in
+        snap(ws.dh, (int64_t)M * D);
         SMC_TRY(ln_bwd_launch(ws.dh, D, ls.x_in, D, ls.mu1, ls.rs1, lw.ln1_w, dx, D, dx, D, M, D, st));
+        snap(dx, (int64_t)M * D);
     }
     // ln_pre backward, drop the class-token row, patch GEMM adjoint, col2im
     SMC_TRY(ln_bwd_launch(dx, D, sv.x_pre, D, sv.mu0, sv.rs0, w.lnpre_w, nullptr, 0, ws.dh, D, M, D, st));
     hipLaunchKernelGGL(embed_bwd_kernel, dim3(ew_blocks((int64_t)Mt * D)), dim3(256), 0, st, ws.dh, ws.tok, B, d.L, D);
     SMC_TRY(smc::check_launch("vit embed bwd"));
+    snap(ws.dh, (int64_t)M * D);
+    snap(ws.tok, (int64_t)Mt * D);
     SMC_TRY(lin(ws.tok, D, w.conv_w, d.P, ws.patches, d.P, Mt, d.P, D, epi_none(), w.conv_w3, w.conv_wt));
+    snap(ws.patches, (int64_t)Mt * d.P);
     return smc_patch_im2col_f32(dimage, ws.patches, B, d.C, d.G, d.p, 1, stream);
 }
