@@ -914,6 +914,24 @@ struct StageSeg {
     float mul;
 };
 
+typedef __attribute__((address_space(3))) float lds_float;
+
+// The segment fields of global float4 index g, selected by compares over the unrolled segment list (constant indices
+// only: a dynamically indexed StageSeg array lives in scratch, and its LDS pointers then come back as generic pointers,
+// so the stores below became flat_store_dwordx4 at 4-B aligned LDS addresses -- the HP = 65 pitch -- which corrupted
+// one dword of a staged float4 now and then while other kernels shared the CU (round 6)).
+template <int NSEG>
+__device__ __forceinline__ void stage_pick(const StageSeg (&s)[NSEG], const int (&start)[NSEG + 1], int g, int& si,
+                                           int& loc) {
+    si = 0;
+#pragma unroll
+    for (int i = 1; i < NSEG; ++i) si = g >= start[i] ? i : si;
+    int base = start[0];
+#pragma unroll
+    for (int i = 1; i < NSEG; ++i) base = si == i ? start[i] : base;
+    loc = g - base;
+}
+
 template <int NSEG, int KMAX>
 __device__ __forceinline__ void stage_segs(const StageSeg (&s)[NSEG]) {
     int start[NSEG + 1];
@@ -925,26 +943,40 @@ __device__ __forceinline__ void stage_segs(const StageSeg (&s)[NSEG]) {
         float4 v[KMAX];
 #pragma unroll
         for (int k = 0; k < KMAX; ++k) {
-            const int g = g0 + (int)threadIdx.x + 256 * k;
-            int si = 0;
+            const int g = min(g0 + (int)threadIdx.x + 256 * k, total - 1);
+            int si, loc;
+            stage_pick<NSEG>(s, start, g, si, loc);
+            const float* src = s[0].src;
+            int64_t ld = s[0].ld;
+            int valid = s[0].valid;
 #pragma unroll
-            for (int i = 1; i < NSEG; ++i) si = g >= start[i] ? i : si;
-            const int loc = min(g, total - 1) - start[si];
-            const int row = min(loc >> 4, s[si].valid - 1);
-            v[k] = *reinterpret_cast<const float4*>(s[si].src + (int64_t)row * s[si].ld + 4 * (loc & 15));
+            for (int i = 1; i < NSEG; ++i) {
+                src = si == i ? s[i].src : src;
+                ld = si == i ? s[i].ld : ld;
+                valid = si == i ? s[i].valid : valid;
+            }
+            const int row = min(loc >> 4, valid - 1);
+            v[k] = *reinterpret_cast<const float4*>(src + (int64_t)row * ld + 4 * (loc & 15));
         }
 #pragma unroll
         for (int k = 0; k < KMAX; ++k) {
             const int g = g0 + (int)threadIdx.x + 256 * k;
             if (g >= total) continue;
-            int si = 0;
+            int si, loc;
+            stage_pick<NSEG>(s, start, g, si, loc);
+            float* dst = s[0].dst;
+            int valid = s[0].valid;
+            float m = s[0].mul;
 #pragma unroll
-            for (int i = 1; i < NSEG; ++i) si = g >= start[i] ? i : si;
-            const int loc = g - start[si];
+            for (int i = 1; i < NSEG; ++i) {
+                dst = si == i ? s[i].dst : dst;
+                valid = si == i ? s[i].valid : valid;
+                m = si == i ? s[i].mul : m;
+            }
             const int row = loc >> 4, c = 4 * (loc & 15);
-            const bool ok = row < s[si].valid;
-            const float m = s[si].mul;
-            float* d = s[si].dst + row * HP + c;
+            const bool ok = row < valid;
+            // dword LDS stores through an LDS-typed pointer (row pitch HP = 65 floats: 4-B alignment only)
+            lds_float* d = (lds_float*)(dst + row * HP + c);
             d[0] = ok ? v[k].x * m : 0.f;
             d[1] = ok ? v[k].y * m : 0.f;
             d[2] = ok ? v[k].z * m : 0.f;

@@ -143,11 +143,20 @@ def main():
                 if trace:
                     off = start
                     for nm, n in names:
-                        a, b = ws0[off:off + n], ws1[off:off + n]
+                        v = 4 * 768 if nm == "head_h" else n   # (the head's rows only)
+                        a, b = ws0[off:off + v], ws1[off:off + v]
                         if not torch.equal(a, b):
                             k = (a != b).nonzero().flatten()
                             msg += (f"; first differing snapshot {nm}: {k.numel()} of {n} elements, first index "
                                     f"{k[0].item()}, max|d| {(a - b).abs().max().item():.2e}")
+                            if nm.endswith("dqkv"):   # [B*L rows][3 * 768]: which rows / columns
+                                rows = sorted(set((k // 2304).tolist()))
+                                cols = (k % 2304)
+                                part = sorted(set((cols // 768).tolist()))
+                                heads = sorted(set(((cols % 768) // 64).tolist()))
+                                dd = sorted(set((cols % 64).tolist()))
+                                msg += (f"\n      rows {rows}\n      q/k/v parts {part} heads {heads} d {dd}"
+                                        f"\n      in-step {a[k[:4]].tolist()} replay {b[k[:4]].tolist()}")
                             break
                         off += n
                 print(msg, flush=True)
