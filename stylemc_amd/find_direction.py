@@ -16,8 +16,9 @@ Landmarks: the reference computes that term under torch.no_grad (:90), so it nev
 direction; a non-zero --landmarks_loss_coef is accepted and ignored with a warning.
 generate_image is called with the missing ``device`` fixed (:309,312 raise TypeError as shipped).
 
-Multi-GPU: every rank draws the same i, takes its contiguous slice of the global batch, and one
-all_reduce(SUM) per step combines the gradient and the loss terms (stylemc_amd.dist).
+Multi-GPU: every rank draws the same i, takes its contiguous slice of the global batch and returns one row per
+image (its gradient and loss terms); one all_gather of those rows (World.gather_rows) and one fixed-order sum over the
+global batch (combine) give every rank the same buffer, bit-equal to the single-process one (stylemc_amd.dist).
 """
 import contextlib
 import math
@@ -491,7 +492,7 @@ class DirectionFinder:
         return self.world.gather_rows(rows, lo, hi).sum(0)
 
     def apply_step(self, buf):
-        """The SGD update from the reduced buffer (every rank holds the same one after the all_reduce)."""
+        """The SGD update from the combined buffer (every rank holds the same one after gather_rows + combine)."""
         lr_t = cosine_lr(self.lr0, self.it, self.total_iterations)
         grad = buf[:-4].view_as(self.delta)
         self.delta = torch.add(self.delta, grad, alpha=-lr_t)  # == torch.optim.SGD step (find_direction.py:339)

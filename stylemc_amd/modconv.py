@@ -97,8 +97,8 @@ class PackedConv:
     def _planes(self, key, wk, cin, cout):
         if key not in self._x3:
             p = x3_planes(wk, cin, cout, enabled=self.use_x3)
-            if p is not None:   # built on this stream, read from any: wait once (first use, i.e. a warm-up step)
-                torch.cuda.current_stream(wk.device).synchronize()
+            if p is not None:   # built on this stream, read from any: wait once (LayerSpec builds the expected ones
+                torch.cuda.current_stream(wk.device).synchronize()   # up front; this is the fallback for others)
             self._x3[key] = p
         return self._x3[key]
 
@@ -284,12 +284,22 @@ class LayerSpec:
             # the spec is built lazily, on whichever stream first reaches the layer (find_direction's first step
             # runs the original-image synthesis on a side stream): build the Winograd transforms of a Winograd
             # layer now, and let every packing kernel finish before another stream can read the packed weights
+            direct = [True, True]   # forward, data gradient on the direct implicit GEMM (split-bf16 planes)
             if resolution is not None and up == 1 and P.k == 3:
                 for flip, (ci, co) in enumerate([(P.cin, P.cout), (P.cout, P.cin)]):
                     if wino4_pick(1, ci, co, resolution, resolution):
                         P.wino4_weights(flip)
+                        direct[flip] = False
                     elif wino_ok(1, ci, co, resolution, resolution):
                         P.wino_weights(flip)
+                        direct[flip] = False
+            # the split-bf16 planes of the directions that take the direct GEMM, built here (one wait below) rather than
+            # on first use inside a step, where the build's host wait would stall whichever stream reached it first
+            if resolution is not None:
+                if direct[0]:
+                    P.x3_fwd if up == 1 else P.x3_phases
+                if direct[1]:
+                    P.x3_bwd
             torch.cuda.current_stream(weight.device).synchronize()
 
 

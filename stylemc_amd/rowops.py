@@ -19,6 +19,8 @@ def row_dot(a, b):
     a = a.contiguous().float()
     b = b.contiguous().float()
     rows, L = a.shape
+    if b.ndim != 2 or b.shape[1] != L or b.shape[0] not in (1, rows):
+        raise ValueError(f"row_dot: b {tuple(b.shape)} must be [1 or {rows}, {L}]")
     out = torch.empty(rows, device=a.device, dtype=torch.float32)
     if rows == 0:
         return out
@@ -75,12 +77,19 @@ def l2_normalize(f):
 
 def direction_head(e, src, t, eps=1e-8):
     """(1 - cos(normalize(e - src), t), d/de) per row in one launch (smc_direction_head_f32); e, src: [R, D], t: [1, D]."""
+    if e.dtype != torch.float32 or src.dtype != torch.float32 or t.dtype != torch.float32:
+        raise ValueError("direction_head: fp32 tensors only")
+    if e.ndim != 2 or src.shape != e.shape or t.shape != (1, e.shape[1]):
+        raise ValueError(f"direction_head: e {tuple(e.shape)}, src {tuple(src.shape)} (same), t {tuple(t.shape)} "
+                         f"(1 x D)")
     e = e if e.stride(-1) == 1 else e.contiguous()
     src = src if src.stride(-1) == 1 else src.contiguous()
     t = t.contiguous()
     rows, D = e.shape
     loss = torch.empty(rows, device=e.device, dtype=torch.float32)
     grad = torch.empty(rows, D, device=e.device, dtype=torch.float32)
+    if rows == 0:
+        return loss, grad
     _hip.call("smc_direction_head_f32", _hip.ptr(e), e.stride(0), _hip.ptr(src), src.stride(0), _hip.ptr(t),
               loss.data_ptr(), grad.data_ptr(), rows, D, float(eps), _hip.stream())
     return loss, grad

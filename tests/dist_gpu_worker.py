@@ -18,10 +18,22 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
-# (global batch, S codes, steps): even shards (4 over 8), uneven 2 + 1 with a short last batch of 1 that leaves
-# rank 1 empty (3 over 7), and rank 1 empty on every step (1 over 3)
-CASES = ((4, 8, 3), (3, 7, 4), (1, 3, 3))
-RES = 256
+# (global batch, S codes, steps[, per-rank batch]): even shards (4 over 8), uneven 2 + 1 with a short last batch of 1
+# that leaves rank 1 empty (3 over 7), and rank 1 empty on every step (1 over 3).  The per-rank batch (default: the
+# global batch) is the finder's batch_size, i.e. the planning batch of every launch (smc_set_plan_batch).
+CASES_BY_RES = {
+    256: ((4, 8, 3), (3, 7, 4), (1, 3, 3)),
+    # the headline configuration (BASELINE configs 2-3): FFHQ-1024 at a global batch of 4 split 2 + 2 (parity mode),
+    # and 4 images per rank (throughput mode: global batch 8, the 1-rank run plans as for 4 images per launch)
+    1024: ((4, 8, 2), (8, 16, 2, 4)),
+}
+RES = int(os.environ.get("SMC_DIST_RES", "256"))
+CASES = CASES_BY_RES[RES]
+
+
+def case(c):
+    """(global batch, S codes, steps, per-rank batch) of a CASES entry."""
+    return (c[0], c[1], c[2], c[3] if len(c) > 3 else c[0])
 
 
 def problem(dev):
@@ -36,11 +48,11 @@ def problem(dev):
     return G, clip, IDLoss(device=dev, weights=None, seed=3), utils.get_temp_shapes(G)
 
 
-def _finder(world, dev, G, clip, idl, shapes, gb, n_items):
+def _finder(world, dev, G, clip, idl, shapes, gb, n_items, bs=None):
     from stylemc_amd import synthetic
     from stylemc_amd.find_direction import DirectionFinder, initial_delta
     styles = synthetic.synthetic_styles(n_items, seed=5).to(dev)
-    f = DirectionFinder(G, styles, clip, idl, resolution=RES, batch_size=gb, global_batch=gb, n_epochs=4,
+    f = DirectionFinder(G, styles, clip, idl, resolution=RES, batch_size=bs or gb, global_batch=gb, n_epochs=4,
                         seed=1, world=world, init_delta=initial_delta(0, 0.01), temp_shapes=shapes)
     assert f.prefetch_orig and f.batch_losses and f._side_stream() is not None, "not the pipelined schedule"
     return f
@@ -57,8 +69,9 @@ def _record(out, gb, f, parts, picks):
 def run_cases(world, dev, G, clip, idl, shapes):
     """Every CASES problem through DirectionFinder.step with `world` (the real N-rank run, or one rank)."""
     out = {}
-    for gb, n_items, steps in CASES:
-        f = _finder(world, dev, G, clip, idl, shapes, gb, n_items)
+    for c in CASES:
+        gb, n_items, steps, bs = case(c)
+        f = _finder(world, dev, G, clip, idl, shapes, gb, n_items, bs)
         parts, picks = [], []
         for _ in range(steps):
             last = f.step()
@@ -74,8 +87,9 @@ def run_cases_simulated(dev, G, clip, idl, shapes, world_size=2):
     order (what the all_gather assembles), every view applies their fixed-order sum (apply_step)."""
     from stylemc_amd import dist as sdist
     out = {}
-    for gb, n_items, steps in CASES:
-        fs = [_finder(sdist.World(r, world_size, 0, None, 0), dev, G, clip, idl, shapes, gb, n_items)
+    for c in CASES:
+        gb, n_items, steps, bs = case(c)
+        fs = [_finder(sdist.World(r, world_size, 0, None, 0), dev, G, clip, idl, shapes, gb, n_items, bs)
               for r in range(world_size)]
         parts, picks = [], []
         for _ in range(steps):
