@@ -218,10 +218,12 @@ def wino4_ok(n, cin, cout, h, w):
 
 
 # F(4x4) where it measured faster than F(2x2) (tools/bench_wino.py, FFHQ-1024 batch 4, profiles/r03_wino4/bench_wino_v2.txt):
-# 1.32-1.35x at cin 512 (r = 64), 1.25-1.27x at 256, 1.14-1.16x at 128, 0.99-1.01x at 64 -- the K loop of a
-# 64-channel input (16 steps) is too short to amortise a work item's fill and output transform.  Module switch.
+# 1.32-1.35x at cin 512 (r = 64), 1.25-1.27x at 256, 1.14-1.16x at 128, 0.99-1.01x at 64 in round 3.  Round 6
+# (profiles/r06/wino4_64/): the r = 512 / 64-channel conv1 now 1.05-1.07x (415 -> 390 us forward, 400 -> 383 data
+# gradient) and the step +1.3 % images/s (three interleaved rounds), so 64-channel inputs take F(4x4) too; the
+# 32-channel r = 1024 layer has no F(4x4) kernel.  Module switch.
 WINO4 = True
-WINO4_MIN_CIN = 128
+WINO4_MIN_CIN = 64
 
 
 def wino4_pick(n, cin, cout, h, w):
