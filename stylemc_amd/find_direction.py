@@ -129,6 +129,12 @@ def cosine_lr(lr0, it, total):
     return float(np.cos(np.pi * it / total) * lr0 * 0.5 + lr0 * 0.5)
 
 
+# The original image's CLIP embeddings computed on the prefetch stream too (CLIP on the critical path then runs the
+# edited half only: forward 4 + backward 4 instead of forward 8 + backward 4).  Module switch for A/B:
+# off -- measured slower again in round 6, 465.5-468.1 against 472.8-475.6 images/s over three interleaved rounds
+# (profiles/r06/prefetch_clip_ab/; round 3: profiles/r03_clip_prefetch_ab.txt).
+PREFETCH_CLIP = False
+
 # The loss composition (find_direction.py:318-330: coefficients x batch sums + the l2 term) as one autograd node with
 # an analytic backward (module switch for A/B): autograd's graph of those scalar ops replays ~20 tiny kernels between
 # the loss heads and the networks' backward, on the step's critical path.
@@ -171,7 +177,7 @@ class DirectionFinder:
                  n_epochs=4, identity_loss_coef=0.6, l2_reg_coef=0.1, clip_loss_coef=1.0, noise_mode="const",
                  seed=0, world=None, global_batch=None, temp_shapes=None, init_delta=None, synth_fn=None,
                  overlap=True, batch_losses=True, prefetch_orig=True, stream_factory=None, G2=None, temp_shapes2=None,
-                 prefetch_id=True, plan_batch=None):
+                 prefetch_id=True, plan_batch=None, prefetch_clip=None):
         self.G = G
         # the edited image's generator (train_latent_mapper.py:100-106,159-162 --network2; default G itself)
         self.G_edit = G2 if G2 is not None else G
@@ -187,6 +193,7 @@ class DirectionFinder:
         # (tools/sensitivity.py: dropping it saves 1.8 ms, dropping CLIP nothing), so its critical-path share is
         # cut to the edited images' forward + backward; CLIP keeps the [edited; original] batch
         self.prefetch_id = prefetch_id
+        self.prefetch_clip = PREFETCH_CLIP if prefetch_clip is None else prefetch_clip
         # Measured and removed (round 4): the original image's CLIP embeddings prefetched too (19.87-20.01 against
         # 19.58-19.71 ms / step, profiles/r03_clip_prefetch_ab.txt), the prefetch replayed as a captured HIP graph
         # (0.7 ms / step slower, profiles/r03_graph_prefetch_ab.txt), the prefetch started after the loss networks'
@@ -452,7 +459,10 @@ class DirectionFinder:
         if self.prefetch_id and getattr(self, "_diag_id_after", None) is not None:
             torch.cuda.current_stream().wait_event(self._diag_id_after)   # diagnostic (tools/det_check.py)
         feats = self.id_loss.target_feats(orig) if self.prefetch_id else None
-        return orig, feats, None
+        embs = None
+        if self.prefetch_clip:
+            embs = [cl.encode_src(s) for (cl, _), (_, s) in zip(self.clip_losses, self._clip_inputs(None, orig))]
+        return orig, feats, embs
 
     def step(self):
         """One iteration: this rank's per-image rows (local_step), the exchange + fixed-order sum (combine), the
