@@ -595,6 +595,390 @@ int64_t wino_split_bytes(int n, int cin, int cout, int h, int w) {
     return ns > 1 ? (((int64_t)ns * n * cout * h * w * 4 + 255) / 256) * 256 : 0;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Split-bf16 F(2x2) for the 32-channel layer (cin = cout = 32: the r = 1024 conv1 forward and its data gradient).
+// The fp32 kernel above spends most of that launch in the fp32 MFMA K loop (219 us of 505 at r = 1024, batch 4:
+// profiles/r06/fir_fwd_ab/README).  Here the 16 per-xi GEMMs run on the bf16 matrix core as three-term splits (the
+// scheme of conv_gemm.hip's x3 kernels: a = a0 + a1 + a2 by truncation, the six products a_i b_j with i + j <= 2,
+// smallest first, error <= 2^-23 |a b| per product): 6 v_mfma_f32_16x16x32_bf16 (16 cycles) per 16x16x32 block in
+// place of 8 v_mfma_f32_16x16x4f32 (32 cycles) -- 2.7x fewer matrix-core cycles.
+//   * the whole K = 32 is one MFMA K block, so a workgroup keeps its image's split U planes in LDS for all its items:
+//     [xi 16][term 3][out block 2][k-octet 4][out 16][8] bf16 = 96 KB (wino_x3_pack_kernel; x s[n, c] folded in for the
+//     style-scaled forward), DMA'd once; an A fragment is one conflict-free ds_read_b128 per term.
+//   * one workgroup per CU (LDS), persistent over the items of one image (grid.y = image; items v, v + gridDim.x, ...),
+//     4 waves x 16 tiles of the item's 2 x 32 tile block.  Lane (tile, k-octet g) transforms the 4 x 4 patches of its
+//     tile for the 8 channels 4 j + g (the read pattern of the fp32 kernel's k-quads: conflict-free), so its B fragment
+//     of every xi -- 8 consecutive MFMA k = channels 4 j + g, j = 0..7 -- is already in its registers; the A planes
+//     store k in the same order.
+//   * one patch buffer: the item's patch is transformed into registers (V[8][16]), then the next item's patch DMA is
+//     issued under this item's MFMAs and epilogue.  The C layout of the 16x16x32 MFMA is the 16x16x4 one, so the
+//     epilogue is the fp32 kernel's.
+// A/B knob: 0 the fp32 kernel for these shapes, 1 the split-bf16 kernel for the conv1 forward form (EK 1), 2 also for
+// the data gradient's (EK 2).
+#ifndef SMC_WINO_X3
+#define SMC_WINO_X3 0
+#endif
+typedef short wbf16x8 __attribute__((ext_vector_type(8)));
+constexpr int X3C = 32;                                   // cin = cout
+constexpr int X3_UPLANE = 16 * 3 * 2 * 4 * 16 * 8;        // bf16 per image
+constexpr int X3_UBYTES = X3_UPLANE * 2;                  // 96 KB
+
+// x = t0 + t1 + t2 for 8 values, as three bf16x8 fragments (the high halves of x, x - t0, x - t0 - t1)
+__device__ __forceinline__ void wx3_split8(const float (&x)[8], wbf16x8 (&t)[3]) {
+    unsigned u0[8], u1[8], u2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const unsigned u = __float_as_uint(x[j]);
+        const float r1 = x[j] - __uint_as_float(u & 0xffff0000u);
+        const unsigned v = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(v & 0xffff0000u);
+        u0[j] = u;
+        u1[j] = v;
+        u2[j] = __float_as_uint(r2);
+    }
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 w0, w1, w2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        w0[j] = __builtin_amdgcn_perm(u0[2 * j + 1], u0[2 * j], 0x07060302u);
+        w1[j] = __builtin_amdgcn_perm(u1[2 * j + 1], u1[2 * j], 0x07060302u);
+        w2[j] = __builtin_amdgcn_perm(u2[2 * j + 1], u2[2 * j], 0x07060302u);
+    }
+    t[0] = __builtin_bit_cast(wbf16x8, w0);
+    t[1] = __builtin_bit_cast(wbf16x8, w1);
+    t[2] = __builtin_bit_cast(wbf16x8, w2);
+}
+
+// out[nn][xi][term][b][g][o16][j] = term of uw[c = 4 j + g][xi / 4][o = 16 b + o16][xi % 4] * (s ? s[nn][c] : 1)
+__global__ __launch_bounds__(256) void wino_x3_pack_kernel(const float* uw, const float* s, short* out, int64_t total) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(e & 7), o16 = (int)((e >> 3) & 15), g = (int)((e >> 7) & 3), b = (int)((e >> 9) & 1);
+        const int xi = (int)((e >> 10) & 15);
+        const int64_t nn = e >> 14;
+        const int c = 4 * j + g, o = 16 * b + o16;
+        float v = uw[((c * 4 + (xi >> 2)) * X3C + o) * 4 + (xi & 3)];
+        if (s) v *= s[nn * X3C + c];
+        const unsigned u = __float_as_uint(v);
+        const float r1 = v - __uint_as_float(u & 0xffff0000u);
+        const unsigned w = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(w & 0xffff0000u);
+        const unsigned term[3] = {u >> 16, w >> 16, __float_as_uint(r2) >> 16};
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+            out[((((nn * 16 + xi) * 3 + t) * 2 + b) * 4 + g) * 128 + o16 * 8 + j] = (short)term[t];
+    }
+}
+
+// (timing probes only, variant libraries: 1 no MFMAs, 2 no epilogue stores, 4 no transform LDS reads, 8 no waits)
+#ifndef SMC_WINO_X3_PROBE
+#define SMC_WINO_X3_PROBE 0
+#endif
+template <int EK>
+__global__ __launch_bounds__(256, 1) void wino_x3_kernel(WinoParams p, const short* planes, int64_t plane_nstride) {
+    static_assert(EK == 1 || EK == 2, "the synthesis' MODACT epilogue forms");
+    using C = WinoCfg<32>;
+    constexpr int TC = 32, TR = C::TR, ROWS = C::ROWS, CH = C::CH, CHP = C::CHP, PITCH = C::PITCH, SLAB = C::SLAB;
+    static_assert(8 * ROWS * CHP == 15 * 64, "a quarter (8 channels) is 15 DMA wave-instructions");
+    constexpr int QF = 16 * 256;                // floats per quarter slot: 15 KB of patch + 1 KB (slot 0: the noise)
+    constexpr int UJW = X3_UBYTES / 1024 / 4;   // U DMA wave-instructions per wave (24)
+    constexpr int OBW = 2;
+    static_assert(X3_UBYTES % 4096 == 0, "U planes split evenly over the 4 waves");
+    __shared__ __attribute__((aligned(16))) char smem[X3_UBYTES + 4 * QF * 4];
+    float* ps = reinterpret_cast<float*>(smem + X3_UBYTES);
+    const float* nsm = ps + 15 * 256;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int H = p.h, W = p.w;
+    const int nn = blockIdx.y;
+    const int items = p.gx * p.gy;
+    const int S = gridDim.x;
+    int k = blockIdx.x;
+    if (k >= items) return;
+    const bool has_noise = p.noise != nullptr, has_u = p.u_save != nullptr;
+    const int kg = lane >> 4;   // MFMA k-octet: channels 4 j + kg
+    const int tl = 16 * wave + (lane & 15);
+    const int tr = tl / TC, tc = tl - tr * TC;
+
+    // the epilogue's per-channel operands, once per workgroup (one image), parked in accumulation registers (the arch
+    // VGPRs hold V, fragments and splits) -- loaded before any DMA, so their wait drains nothing
+    float e_dA[OBW][4], e_bA[OBW][4];
+#pragma unroll
+    for (int b = 0; b < OBW; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int o = 16 * b + 4 * kg + r;
+            const float dv = (p.d ? p.d[(int64_t)nn * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
+            const float bv = p.bias ? p.bias[o] : 0.f;
+            asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(e_dA[b][r]) : "v"(dv));
+            asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(e_bA[b][r]) : "v"(bv));
+        }
+    const float nstr = has_noise ? (p.noise_strength ? *p.noise_strength : 1.f) : 0.f;
+
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * H * W * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ursrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(planes + nn * plane_nstride), (short)0, X3_UBYTES, 0x00020000);
+    const __amdgpu_buffer_rsrc_t nrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.noise, (short)0, has_noise ? (int)(((int64_t)(p.n - 1) * p.noise_nstride + (int64_t)H * W) * 4) : 0,
+        0x00020000);
+#pragma unroll
+    for (int j = 0; j < UJW; ++j) {
+        const int J = wave * UJW + j;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ursrc, (__attribute__((address_space(3))) void*)(smem + J * 1024), 16,
+                                                 (J * 64 + lane) * 16, 0, 0, 0);
+    }
+    // Patch DMA by quarters (8 channels: 15 wave-instructions, + 1: slot 0's 16th is the item's noise [4][64], the others
+    // a zero-fill), every wave exactly 4 per quarter.  The transform reads quarter q of item k while quarters q..3 of
+    // item k + 1 are still to be issued; vmcnt counts loads, stores and LDS-DMA together in issue order, so "quarter q
+    // of k landed" is vmcnt(12 + S): its 3 later quarters, the S epilogue stores of item k - 1, item k + 1's first q.
+    auto dma = [&](int kk, int q) {  // item kk's quarter q (kk >= items: all lanes zero-fill)
+        const bool valid = kk < items;
+        const int ty0 = (kk / p.gx) * TR, tx0 = (kk % p.gx) * TC;
+        float* slot = ps + q * QF;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int jq = wave + 4 * jj;
+            int ln = lane;   // (opaque: the loop-invariant parts of these offsets would be hoisted into 16 registers)
+            asm volatile("" : "+v"(ln));
+            if (jq == 15) {
+                const bool ok = valid && q == 0 && has_noise;
+                const int vo = ok ? ((int)(nn * p.noise_nstride) + (2 * ty0 + (ln >> 4)) * W + 2 * tx0 + 4 * (ln & 15)) * 4
+                                  : 0x7ffffff0;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(nrsrc, (__attribute__((address_space(3))) void*)(slot + 15 * 256),
+                                                         16, vo, 0, 0, 0);
+            } else {
+                const int L = jq * 64 + ln;
+                const int cc = L / (ROWS * CHP);
+                const int r2 = L - cc * (ROWS * CHP);
+                const int r = r2 / CHP, ch = r2 - r * CHP;
+                const int gyy = 2 * ty0 - 1 + r, gxx = 2 * tx0 - 4 + 4 * ch;
+                const bool ok = valid && ch < CH && gyy >= 0 && gyy < H && gxx >= 0 && gxx < W;
+                const int vo = ok ? (((nn * p.cin + 8 * q + cc) * H + gyy) * W + gxx) * 4 : 0x7ffffff0;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (__attribute__((address_space(3))) void*)(slot + jq * 256),
+                                                         16, vo, 0, 0, 0);
+            }
+        }
+    };
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma(k, q);
+
+    // LDS read bases kept opaque so that every fragment / patch read is base + a 16-bit immediate (offsets past 64 KB
+    // would each take a register, hoisted out of the item loop)
+    typedef __attribute__((address_space(3))) const short lds_cshort;
+    typedef __attribute__((address_space(3))) const float lds_cfloat;
+    typedef float f32x2 __attribute__((ext_vector_type(2), aligned(8)));
+    typedef __attribute__((address_space(3))) const f32x2 lds_cf32x2;
+    lds_cshort* ua = (lds_cshort*)smem + (kg * 16 + (lane & 15)) * 8;
+    lds_cshort* ua8 = ua + 8 * 3 * 2 * 512;
+    lds_cfloat* pb = (lds_cfloat*)ps + kg * SLAB + 2 * tr * PITCH + 2 * tc + 2;
+    asm volatile("" : "+v"(ua), "+v"(ua8), "+v"(pb));
+
+    // channel j (= 4 j + kg) of the lane's tile: its 4 x 4 patch from quarter slot j / 2, and V = B^T d B
+    auto transform = [&](int j, float (&vv)[16]) {
+        lds_cfloat* pp = pb + (j >> 1) * QF + (j & 1) * 4 * SLAB;
+        float pd[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if constexpr ((SMC_WINO_X3_PROBE & 4) != 0) {
+                pd[4 * i] = (float)(j + i + tid);
+                pd[4 * i + 1] = pd[4 * i] + 1.f;
+                pd[4 * i + 2] = pd[4 * i] * 3.f;
+                pd[4 * i + 3] = pd[4 * i] - 2.f;
+                continue;
+            }
+            const f32x2 a = *reinterpret_cast<lds_cf32x2*>(pp + i * PITCH);
+            const f32x2 b = *reinterpret_cast<lds_cf32x2*>(pp + i * PITCH + 2);
+            const f32x2 c = *reinterpret_cast<lds_cf32x2*>(pp + i * PITCH + 4);
+            pd[4 * i + 0] = a[1];
+            pd[4 * i + 1] = b[0];
+            pd[4 * i + 2] = b[1];
+            pd[4 * i + 3] = c[0];
+        }
+        float t[4][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            t[0][q] = pd[q] - pd[8 + q];
+            t[1][q] = pd[4 + q] + pd[8 + q];
+            t[2][q] = pd[8 + q] - pd[4 + q];
+            t[3][q] = pd[4 + q] - pd[12 + q];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            vv[4 * i + 0] = t[i][0] - t[i][2];
+            vv[4 * i + 1] = t[i][1] + t[i][2];
+            vv[4 * i + 2] = t[i][2] - t[i][1];
+            vv[4 * i + 3] = t[i][1] - t[i][3];
+        }
+    };
+    auto load_a = [&](int xi, wbf16x8 (&a)[OBW][3]) {
+#pragma unroll
+        for (int b = 0; b < OBW; ++b)
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+                a[b][t] = *reinterpret_cast<__attribute__((address_space(3))) const wbf16x8*>(
+                    (xi < 8 ? ua : ua8) + (((xi & 7) * 3 + t) * 2 + b) * 512);
+    };
+
+    f32x4 acc[16][OBW];
+    for (;;) {
+        const int kn = k + S;
+        // ---- V = B^T d B of item k, quarter by quarter; each freed slot takes item k + 1's quarter at once
+        float V[8][16], nr[2][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if ((SMC_WINO_X3_PROBE & 8) != 0) {}
+            else if (k < (int)blockIdx.x + S) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // (no stores yet)
+            else if (has_u) asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // quarter q landed for every wave; every wave is done with slot q - 1
+            asm volatile("" ::: "memory");
+            if (q > 0) dma(kn, q - 1);
+            if (q == 0) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const f32x2 z = *reinterpret_cast<const f32x2*>(nsm + (2 * tr + i) * 64 + 2 * tc);
+                    nr[i][0] = z[0];
+                    nr[i][1] = z[1];
+                }
+            }
+            transform(2 * q, V[2 * q]);
+            transform(2 * q + 1, V[2 * q + 1]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        dma(kn, 3);
+
+        // ---- M[xi] = U[xi] V[xi]: per xi 2 output blocks x 6 split products; the split (VALU) and A fragment reads of
+        // xi + 1 go between the MFMAs of xi (one wave per SIMD: only its own stream fills the slots an MFMA leaves)
+        auto split = [&](int xi, wbf16x8 (&bt)[3]) {
+            const float xv[8] = {V[0][xi], V[1][xi], V[2][xi], V[3][xi], V[4][xi], V[5][xi], V[6][xi], V[7][xi]};
+            wx3_split8(xv, bt);
+        };
+        wbf16x8 at[2][OBW][3], bt[2][3];
+        load_a(0, at[0]);
+        split(0, bt[0]);
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (xi + 1 < 16) {
+                load_a(xi + 1, at[(xi + 1) & 1]);
+                split(xi + 1, bt[(xi + 1) & 1]);
+            }
+            const wbf16x8 (&a)[OBW][3] = at[xi & 1];
+            const wbf16x8 (&b3)[3] = bt[xi & 1];
+            if constexpr ((SMC_WINO_X3_PROBE & 1) != 0) {
+                acc[xi][0] = f32x4{(float)b3[0][0] + (float)a[0][0][0], (float)b3[1][0], (float)b3[2][0], (float)b3[0][1]};
+                acc[xi][1] = f32x4{(float)b3[0][3] + (float)a[1][2][0], (float)b3[1][4], (float)b3[2][5], (float)b3[2][1]};
+                __builtin_amdgcn_sched_barrier(0);
+                continue;
+            }
+            // four independent chains (each output block: the three small products, the three large ones), each
+            // MFMA four issues after its predecessor in the chain -- two chains left the matrix core waiting on results
+            f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, l0 = s0, l1 = s0;
+            s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][2], b3[0], s0, 0, 0, 0);
+            s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][2], b3[0], s1, 0, 0, 0);
+            l0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][1], b3[0], l0, 0, 0, 0);
+            l1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][1], b3[0], l1, 0, 0, 0);
+            s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][1], b3[1], s0, 0, 0, 0);
+            s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][1], b3[1], s1, 0, 0, 0);
+            l0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][0], b3[1], l0, 0, 0, 0);
+            l1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][0], b3[1], l1, 0, 0, 0);
+            s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][0], b3[2], s0, 0, 0, 0);
+            s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][0], b3[2], s1, 0, 0, 0);
+            l0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][0], b3[0], l0, 0, 0, 0);
+            l1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][0], b3[0], l1, 0, 0, 0);
+            acc[xi][0] = l0 + s0;
+            acc[xi][1] = l1 + s1;
+            if (xi + 1 < 16) {
+#pragma unroll
+                for (int m = 0; m < 12; ++m) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);               // one MFMA
+                    if (m < 6) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // one LDS read
+                    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);               // four VALU
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+
+        // ---- Y = A^T M A per (channel, tile) and the MODACT epilogue (wino_kernel's KIND 1 / 2); 32-bit offsets from
+        // the image's base (64-bit per-row addresses would be hoisted out of the loop into registers it does not have).
+        // Exactly 16 y stores (+ 16 u stores): the vmcnt counts above depend on it.
+        {
+            const int plane = H * W;
+            float* yb = p.y + (int64_t)nn * p.cout * plane;
+            float* ub = has_u ? p.u_save + (int64_t)nn * p.cout * plane : nullptr;
+            const int pix = (2 * ((k / p.gx) * TR + tr)) * W + 2 * ((k % p.gx) * TC + tc) + 4 * kg * plane;
+            float nz[2][2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) nz[i][j] = nr[i][j] * nstr;
+#pragma unroll
+            for (int b = 0; b < OBW; ++b) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float m[4][4];
+#pragma unroll
+                    for (int xi = 0; xi < 16; ++xi) m[xi >> 2][xi & 3] = acc[xi][b][r];
+                    float rr[2][4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        rr[0][j] = m[0][j] + m[1][j] + m[2][j];
+                        rr[1][j] = m[1][j] - m[2][j] - m[3][j];
+                    }
+                    float out[2][2];
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        out[i][0] = rr[i][0] + rr[i][1] + rr[i][2];
+                        out[i][1] = rr[i][1] - rr[i][2] - rr[i][3];
+                    }
+                    float dsc, bo;
+                    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(dsc) : "a"(e_dA[b][r]));
+                    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(bo) : "a"(e_bA[b][r]));
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const int idx = pix + (16 * b + r) * plane + i * W;
+                        if constexpr ((SMC_WINO_X3_PROBE & 2) != 0) {
+                            if (out[i][0] == 12345.f) yb[idx] = out[i][1];
+                            continue;
+                        }
+                        if (has_u) *reinterpret_cast<float2*>(ub + idx) = make_float2(out[i][0], out[i][1]);
+                        float q[2];
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            if constexpr (EK == 1) {
+                                const float z = __fmaf_rn(out[i][j], dsc, nz[i][j]) + bo;
+                                q[j] = smc::lrelu_gain_clamp(z, p.alpha, p.gain, p.clamp);
+                            } else {
+                                q[j] = (__fmaf_rn(out[i][j], dsc, nz[i][j]) + bo) * p.gain;
+                            }
+                        }
+                        *reinterpret_cast<float2*>(yb + idx) = make_float2(q[0], q[1]);
+                    }
+                }
+            }
+        }
+        if (kn >= items) break;
+        k = kn;
+    }
+}
+
+// bytes of split U planes the x3 path takes from the workspace (0: the shape runs the fp32 kernel)
+int64_t wino_x3_bytes(int n, int cin, int cout, int h, int w) {
+    return SMC_WINO_X3 && cin == X3C && cout == X3C && wino_tc(h, w) == 32 ? (int64_t)n * X3_UBYTES : 0;
+}
+
+template <int EK>
+void launch_wino_x3(const WinoParams& p, const short* planes, int64_t nstride, hipStream_t st) {
+    const int items = p.gx * p.gy;
+    const int per_img = (int)std::max<int64_t>(1, std::min<int64_t>(items, smc::device_cu_count() / p.n));
+    hipLaunchKernelGGL(wino_x3_kernel<EK>, dim3((unsigned)per_img, (unsigned)p.n), dim3(256), 0, st, p, planes, nstride);
+}
+
 
 }  // namespace
 
@@ -616,7 +1000,7 @@ SMC_API int smc_wino_weights_f32(const float* w, int cout, int cin, int flip, fl
 // [split-K partial planes (when the grid is too small)][per-image folded U (forward with a style scale)]
 SMC_API int64_t smc_conv3x3_wino_workspace_size(int n, int cin, int cout, int h, int w) {
     if (!smc_conv3x3_wino_supported(n, cin, cout, h, w)) return 0;
-    return wino_split_bytes(n, cin, cout, h, w) + wino_fold_bytes(n, cin, cout);
+    return std::max(wino_split_bytes(n, cin, cout, h, w) + wino_fold_bytes(n, cin, cout), wino_x3_bytes(n, cin, cout, h, w));
 }
 
 SMC_API int smc_conv3x3_wino_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
@@ -661,6 +1045,24 @@ SMC_API int smc_conv3x3_wino_ws_f32(const float* x, int n, int cin, int h, int w
     const int64_t need = smc_conv3x3_wino_workspace_size(n, cin, cout, h, w);
     const int64_t split_bytes = wino_split_bytes(n, cin, cout, h, w), fold_bytes = wino_fold_bytes(n, cin, cout);
     const bool ws_ok = need > 0 && workspace && workspace_bytes >= need;
+    const bool modact_plain = p.mode == SMC_EPI_MODACT && !p.ext.residual;
+    const bool ek1 = modact_plain && p.act == SMC_ACT_LRELU && p.alpha >= 0.f && p.alpha <= 1.f && p.clamp >= 0.f;
+    const bool ek2 = modact_plain && p.act == SMC_ACT_LINEAR && p.clamp < 0.f;
+    const bool noise_ok = !e.noise || ((reinterpret_cast<uintptr_t>(e.noise) & 15) == 0 && e.noise_nstride % 4 == 0);
+    if (wino_x3_bytes(n, cin, cout, h, w) > 0 && ws_ok && noise_ok && (ek1 || (ek2 && SMC_WINO_X3 >= 2))) {
+        // the 32-channel layer on the bf16 matrix core: split U planes (x s[n, c] when scaled) into the workspace
+        SMC_CHECK((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "smc_conv3x3_wino_ws_f32: workspace alignment");
+        short* planes = reinterpret_cast<short*>(workspace);
+        const int64_t total = (int64_t)(s_in ? n : 1) * (X3_UPLANE / 3);
+        hipLaunchKernelGGL(wino_x3_pack_kernel, dim3((unsigned)std::min<int64_t>(smc::ceil_div(total, 256), 4096)),
+                           dim3(256), 0, st, uw, s_in, planes, total);
+        const int rc = smc::check_launch("smc_conv3x3_wino_ws_f32 (x3 planes)");
+        if (rc != SMC_OK) return rc;
+        const int64_t ns = s_in ? X3_UPLANE : 0;
+        if (ek1) launch_wino_x3<1>(p, planes, ns, st);
+        else launch_wino_x3<2>(p, planes, ns, st);
+        return smc::check_launch("smc_conv3x3_wino_ws_f32 (x3)");
+    }
     if (SMC_WINO_FOLD && s_in && fold_bytes > 0 && ws_ok) {
         float* uf = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + split_bytes);
         SMC_CHECK((reinterpret_cast<uintptr_t>(uf) & 15) == 0, "smc_conv3x3_wino_ws_f32: workspace alignment");
@@ -688,10 +1090,9 @@ SMC_API int smc_conv3x3_wino_ws_f32(const float* x, int n, int cin, int h, int w
         return smc_modconv_epilogue_f32(workspace, p.nsplit, p.split_stride, y, n, cout, h, w, &e, stream);
     }
     // the synthesis' two MODACT forms get an epilogue body with the activation fixed at compile time
-    const bool modact_plain = p.mode == SMC_EPI_MODACT && !p.ext.residual;
-    if (modact_plain && p.act == SMC_ACT_LRELU && p.alpha >= 0.f && p.alpha <= 1.f && p.clamp >= 0.f)
+    if (ek1)
         launch_wino_s<1>(s_in != nullptr, tc, p, items, st);
-    else if (modact_plain && p.act == SMC_ACT_LINEAR && p.clamp < 0.f)
+    else if (ek2)
         launch_wino_s<2>(s_in != nullptr, tc, p, items, st);
     else
         launch_wino_s<0>(s_in != nullptr, tc, p, items, st);

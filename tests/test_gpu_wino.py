@@ -237,3 +237,100 @@ def test_wino_unsupported_shapes():
     rc = lib.smc_conv3x3_wino_f32(x.data_ptr(), 1, 32, 16, 16, y.data_ptr(), 32, uw.data_ptr(), None, None,
                                   H.stream())
     assert rc == 2 and b"Winograd" in lib.smc_last_error()
+
+
+# The split-bf16 F(2x2) kernel (wino.hip wino_x3_kernel) is an A/B build option (SMC_AB_DEFINES=SMC_WINO_X3=1); these
+# tests run against such a build (SMC_HIP_LIB) and skip against the product library.
+X3_SHAPES = [  # cin = cout = 32 with 2 x 32 tile blocks (w % 64 == 0, h % 4 == 0): the split-bf16 kernel
+    (2, 32, 32, 64, 64),
+    (1, 32, 32, 128, 256),
+    (3, 32, 32, 68, 128),
+    (4, 32, 32, 1024, 1024),
+]
+
+
+def _x3_ws(n, h, w):
+    nb = _lib().load().smc_conv3x3_wino_workspace_size(n, 32, 32, h, w)
+    if nb != n * 16 * 3 * 2 * 4 * 16 * 8 * 2:   # 96 KB of U planes per image
+        pytest.skip("split-bf16 F(2x2) not enabled in this build (SMC_WINO_X3=0, the default: slower in the full step, "
+                    "profiles/r06/wino_x3/README)")
+    return nb, torch.full((nb // 4,), float("nan"), device=DEV)
+
+
+def _rows_check(got, x64, w64, what, rows=None):
+    if rows is not None:  # the 1024-px case: the first rows of every image (fp64 conv on CPU is slow)
+        got, x64 = got[:, :, :rows], x64[:, :, :rows + 2]
+    ref = F.conv2d(x64, w64, padding=1)
+    bound = F.conv2d(x64.abs(), w64.abs(), padding=1)
+    if rows is not None:
+        ref, bound = ref[:, :, :rows], bound[:, :, :rows]
+    ratio = ((got.double().cpu() - ref).abs() / (bound + 1e-30)).max().item()
+    assert ratio <= TOL, f"{what}: max err / sum|w x| = {ratio:.3e} > {TOL:.1e}"
+
+
+@pytest.mark.parametrize("shape", X3_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_wino_x3_vs_fp64(shape):
+    """The split-bf16 F(2x2) kernel (wino_x3_kernel, taken by the conv1 forward's MODACT form): the style-scaled
+    forward (s folded into per-image planes) and a data-gradient-shaped call (flipped taps, one plane set), through that
+    form with d = 1, no noise, no bias, lrelu slope 1, gain 1 and an unreachable clamp (y = the conv exactly), against
+    fp64 at the fp32 kernel's tolerance TOL -- the three-term products leave out <= 2^-23 |u v| each."""
+    from stylemc_amd import modconv
+    H = _lib()
+    plain = modconv._epilogue(H.EPI_MODACT, None, None, 0, None, None, "lrelu", 1.0, 1.0, 1e30, None)
+    n, cin, cout, h, w = shape
+    g = torch.Generator().manual_seed(13 + sum(shape))
+    x = torch.randn(n, cin, h, w, generator=g)
+    s = torch.rand(n, cin, generator=g) + 0.5
+    W = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    nb, ws = _x3_ws(n, h, w)
+    xd, sd, Wd = x.to(DEV), s.to(DEV), W.to(DEV)
+    rows = 64 if h * w > 1 << 18 else None
+    for flip in (0, 1):
+        uw = torch.empty(16 * cin * cout, device=DEV)
+        H.call("smc_wino_weights_f32", Wd.data_ptr(), cout, cin, flip, uw.data_ptr(), H.stream())
+        y = torch.full((n, cout, h, w), float("nan"), device=DEV)
+        H.call("smc_conv3x3_wino_ws_f32", xd.data_ptr(), n, cin, h, w, y.data_ptr(), cout, uw.data_ptr(),
+               sd.data_ptr() if flip == 0 else None, ctypes.byref(plain), ws.data_ptr(), nb, H.stream())
+        torch.cuda.synchronize()
+        assert torch.isfinite(y).all()
+        if flip == 0:
+            _rows_check(y, x.double() * s.double()[:, :, None, None], W.double(), f"x3 fwd {shape}", rows)
+        else:
+            _rows_check(y, x.double(), W.double().flip(2, 3).transpose(0, 1).contiguous(), f"x3 dgrad {shape}", rows)
+
+
+@pytest.mark.parametrize("act", ["lrelu", "linear"])
+def test_wino_x3_modact_vs_fp32_kernel(act):
+    """The MODACT epilogue through the split-bf16 kernel (workspace) and the fp32 F(2x2) kernel (no workspace): the
+    conv1 forward form (lrelu, gain, clamp, noise, u store) and the data gradient's linear x d form."""
+    from stylemc_amd import modconv
+    H = _lib()
+    n, c, h, w = 2, 32, 64, 128
+    g = torch.Generator().manual_seed(17)
+    W = (torch.randn(c, c, 3, 3, generator=g) / (3 * c ** 0.5)).to(DEV)
+    x = torch.randn(n, c, h, w, generator=g).to(DEV)
+    s = (torch.rand(n, c, generator=g) + 0.5).to(DEV)
+    d = (torch.rand(n, c, generator=g) + 0.5).to(DEV)
+    noise = torch.randn(n, 1, h, w, generator=g).to(DEV)
+    strength = torch.tensor([0.3], device=DEV)
+    bias = torch.randn(c, generator=g).to(DEV)
+    P = modconv.PackedConv(W, 1)
+    nb, ws = _x3_ws(n, h, w)
+    outs = []
+    for use_ws in (True, False):
+        y, u = torch.empty(n, c, h, w, device=DEV), torch.empty(n, c, h, w, device=DEV)
+        if act == "lrelu":
+            epi = modconv._epilogue(H.EPI_MODACT, d, noise, h * w, strength, bias, "lrelu", 0.2, 2 ** 0.5, 1.5, u)
+            sp = s.data_ptr()
+        else:
+            epi = modconv._epilogue(H.EPI_MODACT, d, None, 0, None, None, "linear", 0.0, 1.0, -1.0, u)
+            sp = None
+        H.call("smc_conv3x3_wino_ws_f32", x.data_ptr(), n, c, h, w, y.data_ptr(), c,
+               P.wino_weights(0 if act == "lrelu" else 1).data_ptr(), sp, ctypes.byref(epi),
+               ws.data_ptr() if use_ws else None, nb if use_ws else 0, H.stream())
+        outs.append((y, u))
+    torch.cuda.synchronize()
+    (yx, ux), (yf, uf) = outs
+    assert (ux - uf).abs().max().item() <= 2e-5 * uf.abs().max().item()
+    assert (yx - yf).abs().max().item() <= 1e-4 * yf.abs().max().item()
+    assert ((yx - yf).norm() / yf.norm()).item() <= 1e-6

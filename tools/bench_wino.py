@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-split", action="store_true", help="F(2x2) without split K (modconv.WINO_SPLIT off)")
     ap.add_argument("--res", type=int, nargs="+", default=[32, 64, 128, 256, 512, 1024])
+    ap.add_argument("--modact", action="store_true",
+                    help="the synthesis epilogues (conv1 forward: demod, noise, bias, lrelu, gain, clamp, u store; "
+                         "data gradient: x s) instead of plain stores")
     args = ap.parse_args()
     build.build(verbose=False)
     modconv.WINO_SPLIT = not args.no_split
@@ -53,16 +56,22 @@ def main():
         has4 = modconv.wino4_ok(n, c, c, r, r)
         if has4:
             uf4, ub4 = P.wino4_weights(0), P.wino4_weights(1)
-        st = modconv._epilogue(_hip.EPI_STORE)
+        st = stb = modconv._epilogue(_hip.EPI_STORE)
+        if args.modact:
+            d = torch.rand(n, c, device=dev) + 0.5
+            noise = torch.randn(n, 1, r, r, device=dev)
+            strength, bias, u = torch.tensor([0.3], device=dev), torch.randn(c, device=dev), torch.empty_like(x)
+            st = modconv._epilogue(_hip.EPI_MODACT, d, noise, r * r, strength, bias, "lrelu", 0.2, 2 ** 0.5, 256.0, u)
+            stb = modconv._epilogue(_hip.EPI_MODACT, s, None, 0, None, None, "linear", 0.0, 1.0, -1.0, None)
         runs = {
             ("fwd", "direct"): lambda: modconv.gemm(x, y, phases, nph, c, c, s=s, epi=st),
             ("fwd", "wino"): lambda: modconv.wino(x, y, uf, c, c, s=s, epi=st),
-            ("bwd", "direct"): lambda: modconv.gemm(x, y, bph, bnph, c, c, epi=st),
-            ("bwd", "wino"): lambda: modconv.wino(x, y, ub, c, c, epi=st),
+            ("bwd", "direct"): lambda: modconv.gemm(x, y, bph, bnph, c, c, epi=stb),
+            ("bwd", "wino"): lambda: modconv.wino(x, y, ub, c, c, epi=stb),
         }
         if has4:
             runs[("fwd", "wino4")] = lambda: modconv.wino4(x, y, uf4, c, c, s=s, epi=st)
-            runs[("bwd", "wino4")] = lambda: modconv.wino4(x, y, ub4, c, c, epi=st)
+            runs[("bwd", "wino4")] = lambda: modconv.wino4(x, y, ub4, c, c, epi=stb)
         flops = modconv.conv_flops(n, c, c, r, r, 9)
         wfl = modconv.wino_flops(n, c, c, r, r)
         wfl4 = modconv.wino4_flops(n, c, c, r, r)
