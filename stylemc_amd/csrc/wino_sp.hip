@@ -26,9 +26,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int SBK = 8;     // input channels per K step
 constexpr int SBO = 32;    // output channels per work item
 constexpr int SMAXP = 256; // max floats per plane (16 x 16)
-constexpr int SMAXK = 4;   // max K steps per split
+#ifndef SP_MAXK
+#define SP_MAXK 4
+#endif
+constexpr int SMAXK = SP_MAXK;   // max K steps per split
+// split target: SP_WG_PER_CU workgroups per CU, divided by SP_WG_DIV (A/B knobs)
 #ifndef SP_WG_PER_CU
 #define SP_WG_PER_CU 1
+#endif
+#ifndef SP_WG_DIV
+#define SP_WG_DIV 1
 #endif
 
 struct WspParams {
@@ -283,7 +290,7 @@ SpPlan sp_plan(int n, int cin, int cout, int h, int w) {
     s.nitems = ((n + s.ipi - 1) / s.ipi) * s.ntn;
     // one workgroup per CU (two, i.e. twice the splits, measured 3.38 against 3.25 ms per IR-SE50 f4 + b4: the
     // split-K reduction grows with the splits), whole 8-channel steps per split, at most SMAXK of them
-    const int target = SP_WG_PER_CU * smc::device_cu_count();
+    const int target = SP_WG_PER_CU * smc::device_cu_count() / SP_WG_DIV;
     const int nst = cin / SBK;
     const int plan_items = ((smc::plan_batch(n) + s.ipi - 1) / s.ipi) * s.ntn;   // the split from the planning batch
     s.nsplit = std::min(nst, std::max((int)smc::ceil_div(nst, SMAXK), (int)smc::ceil_div(target, plan_items)));

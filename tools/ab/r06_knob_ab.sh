@@ -9,6 +9,6 @@ for r in $(seq 1 $ROUNDS); do
     i=$((i + 1))
     timeout -k 10 300 python tools/bench_knob.py $v -- --steps 30 --warmup 5 --no-cpu-baseline --no-kernel-timer > $OUT/bench_v${i}_$r.log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "variant $i bench rc=$rc"; tail -5 $OUT/bench_v${i}_$r.log; exit $rc; }
-    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('v$i [$v] round $r:', d['value'], d['ms_per_step'], flush=True)" $OUT/bench_v${i}_$r.log
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('v%s [%s] round %s:' % tuple(sys.argv[2:5]), d['value'], d['ms_per_step'], flush=True)" $OUT/bench_v${i}_$r.log "$i" "$v" "$r"
   done
 done
