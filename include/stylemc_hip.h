@@ -170,6 +170,11 @@ int64_t smc_conv3x3_wino_workspace_size(int n, int cin, int cout, int h, int w);
 int smc_conv3x3_wino_ws_f32(const float* x, int n, int cin, int h, int w, float* y, int cout, const float* uw,
                             const float* s_in, const smc_conv_epilogue* epi, float* workspace, int64_t workspace_bytes,
                             void* stream);
+/* Experimental split-bf16 F(2x2) for cin = cout = 32, w % 64 == 0, h % 4 == 0 (the r = 1024 conv1), taken by
+ * smc_conv3x3_wino_ws_f32 with its workspace when enabled: mode 0 off (the default: slower in the full step,
+ * profiles/r06/wino_x3/README), 1 for the MODACT lrelu form, 2 also for the linear form.  Process-wide; returns the
+ * previous mode.  The workspace size follows the mode in force. */
+int smc_set_wino_x3(int mode);
 /* w [cout][cin][3][3] -> uw [K][4][N][4] floats (16 * cin * cout, 16-B aligned), U = G g G^T per (k, n):
  * flip = 0: K = cin, N = cout, g = w[n][k] (the forward correlation);
  * flip = 1: K = cout, N = cin, g = w[k][n] rotated 180 degrees (the data gradient, conv^T). */

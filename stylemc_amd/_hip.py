@@ -64,6 +64,7 @@ _SIGS = {
     "smc_conv3x3_wino_supported": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "smc_conv3x3_wino_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P]),
     "smc_conv3x3_wino_workspace_size": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
+    "smc_set_wino_x3": (c_int, [c_int]),
     "smc_conv3x3_wino_ws_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, c_int64, P]),
     "smc_wino_weights_f32": (c_int, [P, c_int, c_int, c_int, P, P]),
     "smc_conv3x3_wino4_supported": (c_int, [c_int, c_int, c_int, c_int, c_int]),

@@ -613,11 +613,12 @@ int64_t wino_split_bytes(int n, int cin, int cout, int h, int w) {
 //   * one patch buffer: the item's patch is transformed into registers (V[8][16]), then the next item's patch DMA is
 //     issued under this item's MFMAs and epilogue.  The C layout of the 16x16x32 MFMA is the 16x16x4 one, so the
 //     epilogue is the fp32 kernel's.
-// A/B knob: 0 the fp32 kernel for these shapes, 1 the split-bf16 kernel for the conv1 forward form (EK 1), 2 also for
-// the data gradient's (EK 2).
+// Mode (smc_set_wino_x3, process-wide; SMC_WINO_X3 the build's initial value): 0 the fp32 kernel for these shapes, 1
+// the split-bf16 kernel for the conv1 forward form (EK 1), 2 also for the data gradient's (EK 2).
 #ifndef SMC_WINO_X3
 #define SMC_WINO_X3 0
 #endif
+int g_wino_x3 = SMC_WINO_X3;
 typedef short wbf16x8 __attribute__((ext_vector_type(8)));
 constexpr int X3C = 32;                                   // cin = cout
 constexpr int X3_UPLANE = 16 * 3 * 2 * 4 * 16 * 8;        // bf16 per image
@@ -969,7 +970,7 @@ __global__ __launch_bounds__(256, 1) void wino_x3_kernel(WinoParams p, const sho
 
 // bytes of split U planes the x3 path takes from the workspace (0: the shape runs the fp32 kernel)
 int64_t wino_x3_bytes(int n, int cin, int cout, int h, int w) {
-    return SMC_WINO_X3 && cin == X3C && cout == X3C && wino_tc(h, w) == 32 ? (int64_t)n * X3_UBYTES : 0;
+    return g_wino_x3 && cin == X3C && cout == X3C && wino_tc(h, w) == 32 ? (int64_t)n * X3_UBYTES : 0;
 }
 
 template <int EK>
@@ -981,6 +982,12 @@ void launch_wino_x3(const WinoParams& p, const short* planes, int64_t nstride, h
 
 
 }  // namespace
+
+SMC_API int smc_set_wino_x3(int mode) {
+    const int prev = g_wino_x3;
+    g_wino_x3 = mode < 0 ? 0 : mode > 2 ? 2 : mode;
+    return prev;
+}
 
 SMC_API int smc_conv3x3_wino_supported(int n, int cin, int cout, int h, int w) {
     if (n < 1 || cin < WBK || cin % WBK || cout < WBO || cout % WBO) return 0;
@@ -1049,7 +1056,7 @@ SMC_API int smc_conv3x3_wino_ws_f32(const float* x, int n, int cin, int h, int w
     const bool ek1 = modact_plain && p.act == SMC_ACT_LRELU && p.alpha >= 0.f && p.alpha <= 1.f && p.clamp >= 0.f;
     const bool ek2 = modact_plain && p.act == SMC_ACT_LINEAR && p.clamp < 0.f;
     const bool noise_ok = !e.noise || ((reinterpret_cast<uintptr_t>(e.noise) & 15) == 0 && e.noise_nstride % 4 == 0);
-    if (wino_x3_bytes(n, cin, cout, h, w) > 0 && ws_ok && noise_ok && (ek1 || (ek2 && SMC_WINO_X3 >= 2))) {
+    if (wino_x3_bytes(n, cin, cout, h, w) > 0 && ws_ok && noise_ok && (ek1 || (ek2 && g_wino_x3 >= 2))) {
         // the 32-channel layer on the bf16 matrix core: split U planes (x s[n, c] when scaled) into the workspace
         SMC_CHECK((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "smc_conv3x3_wino_ws_f32: workspace alignment");
         short* planes = reinterpret_cast<short*>(workspace);

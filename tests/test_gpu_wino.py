@@ -239,8 +239,8 @@ def test_wino_unsupported_shapes():
     assert rc == 2 and b"Winograd" in lib.smc_last_error()
 
 
-# The split-bf16 F(2x2) kernel (wino.hip wino_x3_kernel) is an A/B build option (SMC_AB_DEFINES=SMC_WINO_X3=1); these
-# tests run against such a build (SMC_HIP_LIB) and skip against the product library.
+# The split-bf16 F(2x2) kernel (wino.hip wino_x3_kernel) is off in the product; these tests switch it on
+# (smc_set_wino_x3) around each check.
 X3_SHAPES = [  # cin = cout = 32 with 2 x 32 tile blocks (w % 64 == 0, h % 4 == 0): the split-bf16 kernel
     (2, 32, 32, 64, 64),
     (1, 32, 32, 128, 256),
@@ -249,11 +249,19 @@ X3_SHAPES = [  # cin = cout = 32 with 2 x 32 tile blocks (w % 64 == 0, h % 4 == 
 ]
 
 
+@pytest.fixture
+def x3_mode():
+    """The split-bf16 F(2x2) enabled for one test (smc_set_wino_x3; off in the product: slower in the full step,
+    profiles/r06/wino_x3/README)."""
+    lib = _lib().load()
+    prev = lib.smc_set_wino_x3(2)
+    yield
+    lib.smc_set_wino_x3(prev)
+
+
 def _x3_ws(n, h, w):
     nb = _lib().load().smc_conv3x3_wino_workspace_size(n, 32, 32, h, w)
-    if nb != n * 16 * 3 * 2 * 4 * 16 * 8 * 2:   # 96 KB of U planes per image
-        pytest.skip("split-bf16 F(2x2) not enabled in this build (SMC_WINO_X3=0, the default: slower in the full step, "
-                    "profiles/r06/wino_x3/README)")
+    assert nb == n * 16 * 3 * 2 * 4 * 16 * 8 * 2, "not the split-bf16 plan (96 KB of U planes per image)"
     return nb, torch.full((nb // 4,), float("nan"), device=DEV)
 
 
@@ -269,7 +277,7 @@ def _rows_check(got, x64, w64, what, rows=None):
 
 
 @pytest.mark.parametrize("shape", X3_SHAPES, ids=lambda s: "x".join(map(str, s)))
-def test_wino_x3_vs_fp64(shape):
+def test_wino_x3_vs_fp64(shape, x3_mode):
     """The split-bf16 F(2x2) kernel (wino_x3_kernel, taken by the conv1 forward's MODACT form): the style-scaled
     forward (s folded into per-image planes) and a data-gradient-shaped call (flipped taps, one plane set), through that
     form with d = 1, no noise, no bias, lrelu slope 1, gain 1 and an unreachable clamp (y = the conv exactly), against
@@ -300,7 +308,7 @@ def test_wino_x3_vs_fp64(shape):
 
 
 @pytest.mark.parametrize("act", ["lrelu", "linear"])
-def test_wino_x3_modact_vs_fp32_kernel(act):
+def test_wino_x3_modact_vs_fp32_kernel(act, x3_mode):
     """The MODACT epilogue through the split-bf16 kernel (workspace) and the fp32 F(2x2) kernel (no workspace): the
     conv1 forward form (lrelu, gain, clamp, noise, u store) and the data gradient's linear x d form."""
     from stylemc_amd import modconv
