@@ -733,7 +733,9 @@ __global__ __launch_bounds__(256, 1) void wino_x3_kernel(WinoParams p, const sho
     // Patch DMA by quarters (8 channels: 15 wave-instructions, + 1: slot 0's 16th is the item's noise [4][64], the others
     // a zero-fill), every wave exactly 4 per quarter.  The transform reads quarter q of item k while quarters q..3 of
     // item k + 1 are still to be issued; vmcnt counts loads, stores and LDS-DMA together in issue order, so "quarter q
-    // of k landed" is vmcnt(12 + S): its 3 later quarters, the S epilogue stores of item k - 1, item k + 1's first q.
+    // of k landed" is vmcnt(N): its later quarters (12 - 4 q), the S epilogue stores of item k - 1, and item k + 1's
+    // quarters issued so far in this item (4 (q - 1) at q >= 1: quarter q - 1 goes out after quarter q's barrier), so
+    // N = 12 + S at q = 0 and 8 + S after.
     auto dma = [&](int kk, int q) {  // item kk's quarter q (kk >= items: all lanes zero-fill)
         const bool valid = kk < items;
         const int ty0 = (kk / p.gx) * TR, tx0 = (kk % p.gx) * TC;
@@ -830,9 +832,16 @@ __global__ __launch_bounds__(256, 1) void wino_x3_kernel(WinoParams p, const sho
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if ((SMC_WINO_X3_PROBE & 8) != 0) {}
-            else if (k < (int)blockIdx.x + S) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // (no stores yet)
-            else if (has_u) asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+            else if (k < (int)blockIdx.x + S) {   // (no stores yet)
+                if (q == 0) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            } else if (has_u) {
+                if (q == 0) asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+            } else {
+                if (q == 0) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();  // quarter q landed for every wave; every wave is done with slot q - 1
             asm volatile("" ::: "memory");
@@ -968,6 +977,282 @@ __global__ __launch_bounds__(256, 1) void wino_x3_kernel(WinoParams p, const sho
     }
 }
 
+// Register-U form (SMC_WINO_X3R, the default for the split-bf16 path): the 96 KB of U planes left one 256-thread
+// workgroup -- one wave per SIMD -- per CU above, and one wave alone issues a vector instruction every 4 cycles and
+// hides no LDS latency (profiles/r06/wino_x3/README).  Here the waves split the work by Winograd row: an item is one
+// tile row of 32 tiles (a 2 x 64 output block), wave w owns row a = w % 4 (xi = 4 a .. 4 a + 3) of tile block
+// tb = w / 4 (16 tiles), so its A fragments -- 4 xi x 2 output blocks x 3 terms -- fit in registers (the two larger
+// terms, 64 VGPRs; the smallest from a 32 KB LDS copy): 8 waves per workgroup, two per SIMD.  A wave transforms only its
+// row of V (two patch rows per channel); the output transform Y = A^T M A is split the same way -- each wave writes
+// R[a] = M[a][:] A to a 32 KB LDS exchange and, after a barrier, sums the four rows of an eighth of the item's outputs
+// and runs the epilogue.  Patch staging: the quarter ring and counted waits of the kernel above, 16 DMA
+// wave-instructions per quarter (9 of patch, slot 0's 10th the noise rows, the rest zero-fill) = 2 per wave.
+#ifndef SMC_WINO_X3R
+#define SMC_WINO_X3R 1
+#endif
+template <int EK>
+__global__ __launch_bounds__(512, 1) void wino_x3r_kernel(WinoParams p, const short* planes, int64_t plane_nstride) {
+    static_assert(EK == 1 || EK == 2, "the synthesis' MODACT epilogue forms");
+    constexpr int TC = 32, ROWS = 4, CH = TC / 2 + 2, CHP = wino_chp(ROWS, CH), PITCH = 4 * CHP, SLAB = ROWS * PITCH;
+    constexpr int PJ = 8 * ROWS * CHP / 64;   // patch DMA wave-instructions per quarter (9)
+    static_assert(8 * ROWS * CHP == PJ * 64 && PJ < 16, "a quarter's patch is whole wave-instructions, plus the noise");
+    constexpr int QF = 16 * 256;    // floats per quarter slot (16 KB: PJ KB of patch, the noise, zero-fill)
+    constexpr int RINGF = 4 * QF;   // 64 KB
+    constexpr int EXF = 8192;       // exchange: [a 4][tb 2][b 2][r 4][lane 64][2] floats = 32 KB
+    __shared__ __attribute__((aligned(16))) char smem[RINGF * 4 + EXF * 4 + 32768];
+    float* ps = reinterpret_cast<float*>(smem);
+    const float* nsm = ps + PJ * 256;   // slot 0: the item's noise rows [2][64]
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ra = wave & 3, tb = wave >> 2;   // this wave's Winograd row a and tile block
+    const int H = p.h, W = p.w;
+    const int nn = blockIdx.y;
+    const int items = p.gx * p.gy;
+    const int SG = gridDim.x;
+    int k = blockIdx.x;
+    if (k >= items) return;
+    const bool has_noise = p.noise != nullptr, has_u = p.u_save != nullptr;
+    const int kg = lane >> 4, o16 = lane & 15;
+    // combine role: tile block ctb, output block cb, rows r = 2 crp, 2 crp + 1 of the lane's k-octet
+    const int ctb = wave >> 2, cb = (wave >> 1) & 1, crp = wave & 1;
+
+    // epilogue operands and the two larger U terms of this wave's row, loaded and consumed before any DMA (a later first
+    // use would make the compiler wait for the DMAs)
+    float e_d[2], e_b[2];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const int o = 16 * cb + 4 * kg + 2 * crp + rr;
+        e_d[rr] = (p.d ? p.d[(int64_t)nn * p.cout + o] : 1.f) * (p.ext.scale_c ? p.ext.scale_c[o] : 1.f);
+        e_b[rr] = p.bias ? p.bias[o] : 0.f;
+    }
+    const float nstr = has_noise ? (p.noise_strength ? *p.noise_strength : 1.f) : 0.f;
+    const short* up = planes + nn * plane_nstride;
+    wbf16x8 ua0[4][2], ua1[4][2];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int xi = 4 * ra + x;
+            ua0[x][b] = *reinterpret_cast<const wbf16x8*>(up + (((xi * 3 + 0) * 2 + b) * 4 + kg) * 128 + o16 * 8);
+            ua1[x][b] = *reinterpret_cast<const wbf16x8*>(up + (((xi * 3 + 1) * 2 + b) * 4 + kg) * 128 + o16 * 8);
+        }
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) asm volatile("" ::"v"(e_d[rr]), "v"(e_b[rr]));
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) asm volatile("" ::"v"(ua0[x][b]), "v"(ua1[x][b]));
+
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.x, (short)0, (int)((int64_t)p.n * p.cin * H * W * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ursrc = __builtin_amdgcn_make_buffer_rsrc((void*)up, (short)0, X3_UBYTES, 0x00020000);
+    const __amdgpu_buffer_rsrc_t nrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.noise, (short)0, has_noise ? (int)(((int64_t)(p.n - 1) * p.noise_nstride + (int64_t)H * W) * 4) : 0,
+        0x00020000);
+    // the smallest term: block J = 2 xi + b is the planes' [kg 4][o16 16][8] run of term 2 -- 1 KB, one DMA each
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+        const int J = wave + 8 * jj;
+        const int xi = J >> 1, b = J & 1;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            ursrc, (__attribute__((address_space(3))) void*)(smem + RINGF * 4 + EXF * 4 + J * 1024), 16,
+            ((((xi * 3 + 2) * 2 + b) * 512) + lane * 8) * 2, 0, 0, 0);
+    }
+    auto dma = [&](int kk, int q) {  // item kk's quarter q: 16 wave-instructions, 2 per wave (kk >= items: zero-fill)
+        const bool valid = kk < items;
+        const int ty0 = kk / p.gx, tx0 = (kk % p.gx) * TC;
+        float* slot = ps + q * QF;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int jq = wave + 8 * jj;
+            int ln = lane;   // (opaque: keeps the loop-invariant parts of the offsets out of registers)
+            asm volatile("" : "+v"(ln));
+            if (jq >= PJ) {  // the noise (slot 0) / zero-fill
+                const bool ok = valid && q == 0 && jq == PJ && has_noise && ln < 32;
+                const int vo = ok ? ((int)(nn * p.noise_nstride) + (2 * ty0 + (ln >> 4)) * W + 2 * tx0 + 4 * (ln & 15)) * 4
+                                  : 0x7ffffff0;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(nrsrc, (__attribute__((address_space(3))) void*)(slot + jq * 256),
+                                                         16, vo, 0, 0, 0);
+            } else {
+                const int L = jq * 64 + ln;
+                const int cc = L / (ROWS * CHP);
+                const int r2 = L - cc * (ROWS * CHP);
+                const int r = r2 / CHP, ch = r2 - r * CHP;
+                const int gyy = 2 * ty0 - 1 + r, gxx = 2 * tx0 - 4 + 4 * ch;
+                const bool ok = valid && ch < CH && gyy >= 0 && gyy < H && gxx >= 0 && gxx < W;
+                const int vo = ok ? (((nn * p.cin + 8 * q + cc) * H + gyy) * W + gxx) * 4 : 0x7ffffff0;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (__attribute__((address_space(3))) void*)(slot + jq * 256),
+                                                         16, vo, 0, 0, 0);
+            }
+        }
+    };
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma(k, q);
+
+    typedef __attribute__((address_space(3))) const float lds_cfloat;
+    typedef float f32x2 __attribute__((ext_vector_type(2), aligned(8)));
+    typedef __attribute__((address_space(3))) const f32x2 lds_cf32x2;
+    typedef __attribute__((address_space(3))) f32x2 lds_f32x2;
+    typedef __attribute__((address_space(3))) const wbf16x8 lds_cbf16x8;
+    // the row pair of this wave's Winograd row: t[a] = d[r0] + sg d[r1] (B^T rows 1 0 -1 0 / 0 1 1 0 / 0 -1 1 0 /
+    // 0 1 0 -1); the 16 tiles' columns are 2 tc + 2 .. 2 tc + 7 of the staged rows
+    const int r0 = ra == 0 ? 0 : ra == 2 ? 2 : 1;
+    const int r1 = ra == 0 ? 2 : ra == 2 ? 1 : ra == 1 ? 2 : 3;
+    const float sg = ra == 1 ? 1.f : -1.f;
+    lds_cfloat* pb = (lds_cfloat*)ps + kg * SLAB + 2 * (16 * tb + o16) + 2;
+    lds_cfloat* pr0 = pb + r0 * PITCH;
+    lds_cfloat* pr1 = pb + r1 * PITCH;
+    lds_cbf16x8* a2p = (lds_cbf16x8*)(smem + RINGF * 4 + EXF * 4) + (8 * ra) * 64 + lane;   // + (2 x + b) * 64
+    lds_f32x2* exw = (lds_f32x2*)(ps + RINGF) + (ra * 2 + tb) * 2 * 4 * 64 + lane;          // + (b 4 + r) 64
+    lds_cf32x2* exr = (lds_cf32x2*)(ps + RINGF) + (ctb * 2 + cb) * 4 * 64 + 2 * crp * 64 + lane;  // + a 1024 + rr 64
+    asm volatile("" : "+v"(pr0), "+v"(pr1), "+v"(a2p), "+v"(exw), "+v"(exr));
+
+    auto row = [&](lds_cfloat* pp, float (&d)[4]) {
+        const f32x2 a = *reinterpret_cast<lds_cf32x2*>(pp);
+        const f32x2 b = *reinterpret_cast<lds_cf32x2*>(pp + 2);
+        const f32x2 c = *reinterpret_cast<lds_cf32x2*>(pp + 4);
+        d[0] = a[1];
+        d[1] = b[0];
+        d[2] = b[1];
+        d[3] = c[0];
+    };
+
+    for (;;) {
+        const int kn = k + SG;
+        // ---- this wave's row of V = B^T d B, quarter by quarter
+        float V[8][4], nr[2][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            // quarter q of item k landed: all but its later quarters (6 - 2 q), the S stores of item k - 1 and the
+            // 2 (q - 1) DMAs of item k + 1 issued at quarters 1 .. q - 1 -- N = 6 + S at q = 0, 4 + S after
+            if (k < (int)blockIdx.x + SG) {   // (no stores yet)
+                if (q == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            } else if (has_u) {
+                if (q == 0) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            } else {
+                if (q == 0) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();   // quarter q landed for every wave; slot q - 1 and the exchange are free
+            asm volatile("" ::: "memory");
+            if (q > 0) dma(kn, q - 1);
+            if (q == 0) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const f32x2 z = *reinterpret_cast<const f32x2*>(nsm + i * 64 + 2 * (16 * ctb + o16));
+                    nr[i][0] = z[0];
+                    nr[i][1] = z[1];
+                }
+            }
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                const int off = q * QF + jj * 4 * SLAB;
+                float d0[4], d1[4], t[4];
+                row(pr0 + off, d0);
+                row(pr1 + off, d1);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) t[c] = d0[c] + sg * d1[c];
+                float* v = V[2 * q + jj];
+                v[0] = t[0] - t[2];
+                v[1] = t[1] + t[2];
+                v[2] = t[2] - t[1];
+                v[3] = t[1] - t[3];
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        dma(kn, 3);
+
+        // ---- M[a][x] = U[4a + x] V[4a + x] (4 independent chains per x), then R[a] = M[a][:] A into the exchange
+        {
+            f32x4 acc[4][2];
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                const float xv[8] = {V[0][x], V[1][x], V[2][x], V[3][x], V[4][x], V[5][x], V[6][x], V[7][x]};
+                wbf16x8 bt[3];
+                wx3_split8(xv, bt);
+                const wbf16x8 a2_0 = a2p[(2 * x + 0) * 64], a2_1 = a2p[(2 * x + 1) * 64];
+                f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, l0 = s0, l1 = s0;
+                s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2_0, bt[0], s0, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2_1, bt[0], s1, 0, 0, 0);
+                l0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua1[x][0], bt[0], l0, 0, 0, 0);
+                l1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua1[x][1], bt[0], l1, 0, 0, 0);
+                s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua1[x][0], bt[1], s0, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua1[x][1], bt[1], s1, 0, 0, 0);
+                l0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua0[x][0], bt[1], l0, 0, 0, 0);
+                l1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua0[x][1], bt[1], l1, 0, 0, 0);
+                s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua0[x][0], bt[2], s0, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua0[x][1], bt[2], s1, 0, 0, 0);
+                l0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua0[x][0], bt[0], l0, 0, 0, 0);
+                l1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua0[x][1], bt[0], l1, 0, 0, 0);
+                acc[x][0] = l0 + s0;
+                acc[x][1] = l1 + s1;
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float m0 = acc[0][b][r], m1 = acc[1][b][r], m2 = acc[2][b][r], m3 = acc[3][b][r];
+                    exw[(b * 4 + r) * 64] = f32x2{m0 + m1 + m2, m1 - m2 - m3};
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();   // every row's R is in the exchange
+        asm volatile("" ::: "memory");
+
+        // ---- Y = A^T R (rows 1 1 1 0 / 0 1 -1 -1) for tile block ctb, output block cb, rows 2 crp .. + 1; the
+        // epilogue.  Exactly 4 y stores (+ 4 u stores) per wave: the vmcnt counts above depend on it.
+        {
+            const int plane = H * W;
+            float* yb = p.y + (int64_t)nn * p.cout * plane;
+            float* ub = has_u ? p.u_save + (int64_t)nn * p.cout * plane : nullptr;
+            const int pix = (2 * (k / p.gx)) * W + 2 * ((k % p.gx) * TC + 16 * ctb + o16) +
+                            (16 * cb + 4 * kg + 2 * crp) * plane;
+            float nz[2][2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) nz[i][j] = nr[i][j] * nstr;
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                f32x2 R[4];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) R[a] = exr[a * 1024 + rr * 64];
+                float out[2][2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    out[0][j] = R[0][j] + R[1][j] + R[2][j];
+                    out[1][j] = R[1][j] - R[2][j] - R[3][j];
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int idx = pix + rr * plane + i * W;
+                    if (has_u) *reinterpret_cast<float2*>(ub + idx) = make_float2(out[i][0], out[i][1]);
+                    float qv[2];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        if constexpr (EK == 1) {
+                            const float z = __fmaf_rn(out[i][j], e_d[rr], nz[i][j]) + e_b[rr];
+                            qv[j] = smc::lrelu_gain_clamp(z, p.alpha, p.gain, p.clamp);
+                        } else {
+                            qv[j] = (__fmaf_rn(out[i][j], e_d[rr], nz[i][j]) + e_b[rr]) * p.gain;
+                        }
+                    }
+                    *reinterpret_cast<float2*>(yb + idx) = make_float2(qv[0], qv[1]);
+                }
+            }
+        }
+        if (kn >= items) break;
+        k = kn;
+    }
+}
+
 // bytes of split U planes the x3 path takes from the workspace (0: the shape runs the fp32 kernel)
 int64_t wino_x3_bytes(int n, int cin, int cout, int h, int w) {
     return g_wino_x3 && cin == X3C && cout == X3C && wino_tc(h, w) == 32 ? (int64_t)n * X3_UBYTES : 0;
@@ -977,7 +1262,14 @@ template <int EK>
 void launch_wino_x3(const WinoParams& p, const short* planes, int64_t nstride, hipStream_t st) {
     const int items = p.gx * p.gy;
     const int per_img = (int)std::max<int64_t>(1, std::min<int64_t>(items, smc::device_cu_count() / p.n));
-    hipLaunchKernelGGL(wino_x3_kernel<EK>, dim3((unsigned)per_img, (unsigned)p.n), dim3(256), 0, st, p, planes, nstride);
+    if (SMC_WINO_X3R) {   // items of one tile row (32 tiles)
+        WinoParams q = p;
+        q.gy = p.h / 2;
+        const int per = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)q.gx * q.gy, smc::device_cu_count() / p.n));
+        hipLaunchKernelGGL(wino_x3r_kernel<EK>, dim3((unsigned)per, (unsigned)p.n), dim3(512), 0, st, q, planes, nstride);
+    } else
+        hipLaunchKernelGGL(wino_x3_kernel<EK>, dim3((unsigned)per_img, (unsigned)p.n), dim3(256), 0, st, p, planes,
+                           nstride);
 }
 
 

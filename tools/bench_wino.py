@@ -35,12 +35,14 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-split", action="store_true", help="F(2x2) without split K (modconv.WINO_SPLIT off)")
     ap.add_argument("--res", type=int, nargs="+", default=[32, 64, 128, 256, 512, 1024])
+    ap.add_argument("--x3", type=int, default=0, help="smc_set_wino_x3 mode (the split-bf16 F(2x2) for 32 channels)")
     ap.add_argument("--modact", action="store_true",
                     help="the synthesis epilogues (conv1 forward: demod, noise, bias, lrelu, gain, clamp, u store; "
                          "data gradient: x s) instead of plain stores")
     args = ap.parse_args()
     build.build(verbose=False)
     modconv.WINO_SPLIT = not args.no_split
+    _hip.load().smc_set_wino_x3(args.x3)
     n, dev = args.batch, "cuda"
     tot = {"direct": 0.0, "wino": 0.0, "wino4": 0.0}
     for r in args.res:
