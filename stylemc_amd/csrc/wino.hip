@@ -43,6 +43,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef SMC_WINO_ZEROC
 #define SMC_WINO_ZEROC 0
 #endif
+// cache-policy bits of the input patch DMAs (A/B knob; 2 = nt)
+#ifndef SMC_WINO_XAUX
+#define SMC_WINO_XAUX 0
+#endif
 
 constexpr int WBK = 8;    // input channels per K step
 constexpr int WBO = 32;   // output channels per workgroup
@@ -199,7 +203,8 @@ void wino_kernel(WinoParams p) {
             if (wave + NW * jj < C::PJ) {
                 const int vo = pv[jj];
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    xrsrc, (__attribute__((address_space(3))) void*)(ps + (wave + NW * jj) * 256), 16, vo, pso, 0, 0);
+                    xrsrc, (__attribute__((address_space(3))) void*)(ps + (wave + NW * jj) * 256), 16, vo, pso, 0,
+                    SMC_WINO_XAUX);
             }
     };
 
