@@ -1987,10 +1987,12 @@ int validate(const float* x, int n, int cin, int in_h, int in_w, float* y, int c
 namespace {
 
 // Split-K target of the IR-SE50 executor's GEMMs (TAG 1), in workgroups per CU: its 7..28-px stages are
-// latency-bound chains of small GEMMs where more, shorter splits pay (tools/prof_irse.py, IR-SE50 pair
-// fwd(8) + bwd(4): 2 -> 4.34 ms, 4 -> 4.16; 1 -> 4.99).  The synthesis keeps 2.
+// latency-bound chains of small GEMMs where more, shorter splits pay alone (tools/prof_irse.py, IR-SE50 pair
+// fwd(8) + bwd(4): 2 -> 4.34 ms, 4 -> 4.16; 1 -> 4.99) -- but in the pipelined step, beside the CLIP tower on the
+// main stream, 2 is faster: 470.5 / 470.1 / 469.9 / 471.0 against 467.6 / 468.6 / 468.0 / 467.8 images/s over four
+// interleaved rounds (+0.5 %, and ahead in all 3 rounds of a first A/B; 8 slower; profiles/r06/irse_aux_split_ab/).
 #ifndef SMC_AUX_SPLIT_PER_CU
-#define SMC_AUX_SPLIT_PER_CU 4
+#define SMC_AUX_SPLIT_PER_CU 2
 #endif
 constexpr int kSplitPerCuAux = SMC_AUX_SPLIT_PER_CU;
 
