@@ -1989,10 +1989,11 @@ namespace {
 // Split-K target of the IR-SE50 executor's GEMMs (TAG 1), in workgroups per CU: its 7..28-px stages are
 // latency-bound chains of small GEMMs where more, shorter splits pay alone (tools/prof_irse.py, IR-SE50 pair
 // fwd(8) + bwd(4): 2 -> 4.34 ms, 4 -> 4.16; 1 -> 4.99) -- but in the pipelined step, beside the CLIP tower on the
-// main stream, 2 is faster: 470.5 / 470.1 / 469.9 / 471.0 against 467.6 / 468.6 / 468.0 / 467.8 images/s over four
-// interleaved rounds (+0.5 %, and ahead in all 3 rounds of a first A/B; 8 slower; profiles/r06/irse_aux_split_ab/).
+// main stream, fewer splits leave the main stream more of the chip: 2 beat 4 in all 7 rounds of two interleaved
+// A/Bs (+0.5 %), then 1 beat 2 in all 7 rounds of two more (+0.8 % and +1.6 %; 3 and 8 slower):
+// profiles/r06/irse_aux_split_ab/.
 #ifndef SMC_AUX_SPLIT_PER_CU
-#define SMC_AUX_SPLIT_PER_CU 2
+#define SMC_AUX_SPLIT_PER_CU 1
 #endif
 constexpr int kSplitPerCuAux = SMC_AUX_SPLIT_PER_CU;
 
