@@ -1990,10 +1990,11 @@ namespace {
 // latency-bound chains of small GEMMs where more, shorter splits pay alone (tools/prof_irse.py, IR-SE50 pair
 // fwd(8) + bwd(4): 2 -> 4.34 ms, 4 -> 4.16; 1 -> 4.99) -- but in the pipelined step, beside the CLIP tower on the
 // main stream, fewer splits leave the main stream more of the chip: 2 beat 4 in all 7 rounds of two interleaved
-// A/Bs (+0.5 %), then 1 beat 2 in all 7 rounds of two more (+0.8 % and +1.6 %; 3 and 8 slower):
-// profiles/r06/irse_aux_split_ab/.
+// A/Bs (+0.5 %).  1 beat 2 in all 7 rounds of two more (+0.8 % and +1.6 %) but moves the IR-SE50 input gradient of
+// the one-face fp64 test to 2.9e-3 of its max (the bound is 1e-3 there: the reference's fp32 path is 1e-6 away), so
+// it is not used (profiles/r06/irse_aux_split_ab/).
 #ifndef SMC_AUX_SPLIT_PER_CU
-#define SMC_AUX_SPLIT_PER_CU 1
+#define SMC_AUX_SPLIT_PER_CU 2
 #endif
 constexpr int kSplitPerCuAux = SMC_AUX_SPLIT_PER_CU;
 
